@@ -1,0 +1,201 @@
+"""bench.py — similarity queries/sec + p50 latency on MI355X (BASELINE.json `metric`).
+
+Workload (configs[1]): batch of 256 query embeddings × 25,216 × 384-d item matrix, exact
+cosine top-50, one MI355X per rank.  A step = one bb_search over one batch with the item
+matrix and the queries already resident in HBM (prep -> MFMA score slab -> top-K select
+-> finalize).  At 25K items the index does not shard: with --gpus N every
+rank serves its own batch against a full replica ("replicas only", weak scaling, no
+collective on the data path); value = queries of all ranks / max-over-ranks wall time.
+
+Launch: python bench.py [--gpus 1 --steps 500 --warmup 50]
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "brickbrain-rec-engine_amd"))
+
+N_ITEMS, DIM, BATCH, TOPK = 25216, 384, 256, 50
+PEAK = {"f32": ("mfma", 157.3, "TFLOP/s"), "bf16": ("mfma", 2500.0, "TFLOP/s")}
+HBM_PEAK_GBS = 8000.0
+
+
+def unit_rows_torch(n, d, seed, device):
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    x = torch.randn((n, d), generator=g, device=device, dtype=torch.float32)
+    return x / x.norm(dim=1, keepdim=True)
+
+
+def load_pmc(dtype):
+    """HBM bytes per dominant-kernel launch from the committed rocprofv3 PMC summary."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get(dtype, {}).get("gemm")
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(x_np, q_np, k, budget_s=10.0, max_batches=400):
+    """The oracle's batched exact cosine top-k (numpy/BLAS) on the host cores."""
+    from oracle.restatement import batched_cosine_topk
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    batched_cosine_topk(x_np, q_np[:8], k)  # warm BLAS
+    t0 = time.perf_counter()
+    nb = 0
+    lat = []
+    ids0 = None
+    while nb < max_batches and time.perf_counter() - t0 < budget_s:
+        t1 = time.perf_counter()
+        ids, sc = batched_cosine_topk(x_np, q_np, k)
+        lat.append(time.perf_counter() - t1)
+        if ids0 is None:
+            ids0 = ids
+        nb += 1
+    el = time.perf_counter() - t0
+    return {"value": round(nb * q_np.shape[0] / el, 1), "unit": "queries/s", "cores": int(cores),
+            "kind": "port", "p50_ms": round(1e3 * float(np.median(lat)), 3),
+            "sample": f"{nb} batches x {q_np.shape[0]} queries x {x_np.shape[0]} x {x_np.shape[1]} fp32 "
+                      f"(numpy/BLAS restatement, oracle/restatement.py batched_cosine_topk)"}, ids0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import brickrec
+    B = args.batch
+    x = unit_rows_torch(N_ITEMS, DIM, 1234, dev)              # replica of the item matrix
+    q = unit_rows_torch(B, DIM, 4321 + rank, dev)              # this rank's batch
+    idx = brickrec.ItemIndex(device=local, dtype=args.dtype)
+    idx.upload_items(x)
+    stream = torch.cuda.current_stream(dev)
+    run, (o_sc, o_ids, o_cnt) = idx.prepared_search("semantic", TOPK, q_rows=q, stream=stream)
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+
+    # ---- timed region: K steps, barrier + sync on both sides, max over ranks ----
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        run()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    lat_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+
+    # ---- per-kernel device time (HIP events on the launch stream), same K steps ----
+    idx.set_profiling(True)
+    for _ in range(args.steps):
+        run()
+    prof = idx.profile()
+    idx.set_profiling(False)
+    g = prof["gemm"]
+    gemm_us = 1e3 * g["ms"] / max(g["launches"], 1)
+    flops = 2.0 * B * N_ITEMS * DIM
+    es = 4 if args.dtype == "f32" else 2
+    alg_bytes = N_ITEMS * DIM * es + B * DIM * es + B * N_ITEMS * 4  # items + queries + score slab
+    bound, peak, unit = PEAK[args.dtype]
+    achieved = flops / (gemm_us * 1e-6) / 1e12
+    hbm = load_pmc(args.dtype)
+
+    # ---- MALL-cold latency (256 MiB Infinity Cache flushed before each step) ----
+    flush = torch.empty(640 << 20, dtype=torch.uint8, device=dev)
+    cold = []
+    for i in range(20):
+        flush.fill_(i & 0xFF)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        run()
+        b.record(stream)
+        torch.cuda.synchronize()
+        cold.append(a.elapsed_time(b))
+    del flush
+
+    out = {
+        "metric": "similarity queries/sec + p50 latency, 384-d x 25,216 items (configs[1])",
+        "value": round(world * B * args.steps / el, 1),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * el / args.steps, 4),
+        "p50_ms": round(float(np.median(lat_ms)), 4),
+        "p50_ms_mall_cold": round(float(np.median(cold)), 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (unit-norm N(0,1) rows, seeds 1234 / 4321+rank)",
+        "config": {"workload": "configs[1]: batch=256 queries x 25,216 x 384-d items, cosine top-50",
+                   "items": N_ITEMS, "dim": DIM, "batch": B, "top_k": TOPK,
+                   "parallelism": f"replicas x{world}" if world > 1 else "single"},
+        "roofline": {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+                     "frac": round(achieved / peak, 4), "traffic": hbm,
+                     "kernel": "gemm_nt_kernel", "kernel_us": round(gemm_us, 3),
+                     "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": alg_bytes,
+                     "hbm_frac_at_alg_bytes": round(alg_bytes / (gemm_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
+        "kernels_us_per_step": {k: round(1e3 * v["ms"] / max(args.steps, 1), 3) for k, v in prof.items()
+                                if v["launches"]},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        x_np = x.cpu().numpy()
+        q_np = q.cpu().numpy()
+        cb, ids0 = cpu_baseline(x_np, q_np, TOPK)
+        gpu_ids = o_ids.cpu().numpy()
+        same = float(np.mean([set(gpu_ids[i]) == set(ids0[i]) for i in range(B)]))
+        cb["topk_set_agreement_with_gpu"] = round(same, 4)
+        out["cpu_baseline"] = cb
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

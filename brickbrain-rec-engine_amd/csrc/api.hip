@@ -1,0 +1,639 @@
+// api.hip — libbrickrec C-ABI: index handle, uploads, batched search, cross-shard finalize.
+//
+// Search pipeline per query chunk (all stream-ordered, no host sync unless results are host):
+//   prep (normalise / gather / copy query rows)
+//   for each side (content/semantic = cosine over the item matrix; CF = u·F):
+//     for each item slab:  gemm (MFMA score slab) -> select (exact top-K_int, carried list)
+//   finalize (rank-0 drop, truncation, hybrid union-blend) -> scores / ids / counts
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/brickrec.h"
+#include "common.h"
+
+using namespace bb;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define BB_HIP(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t e__ = (expr);                                                                 \
+    if (e__ != hipSuccess)                                                                   \
+      return fail(BB_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e__));           \
+  } while (0)
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+size_t elem_size(int dtype) { return dtype == F64 ? 8 : dtype == BF16 ? 2 : 4; }
+
+enum Kfam { K_PREP = 0, K_GEMM = 1, K_SELECT = 2, K_FIN = 3, K_MASK = 4, K_NFAM = 5 };
+const char* kFamNames[K_NFAM] = {"prep", "gemm", "select", "finalize", "mask"};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return BB_OK;
+    if (p) {
+      hipError_t e = hipFree(p);
+      if (e != hipSuccess) return fail(BB_E_HIP, std::string("hipFree: ") + hipGetErrorString(e));
+      p = nullptr;
+      cap = 0;
+    }
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return fail(BB_E_NOMEM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    }
+    cap = bytes;
+    return BB_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct bb_index {
+  int device = 0;
+  int dtype = F32;
+  int64_t id_offset = 0;
+  int64_t ws_cap = 512ll << 20;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+
+  int64_t n = 0, Npad = 0;
+  int d = 0, Dpad = 0;
+  DevBuf items, items_present;
+  int r = 0, Rpad = 0;
+  DevBuf cf, cf_present;
+  DevBuf parts, year, theme;
+
+  // workspace
+  DevBuf qn, qcf, S, keys, maxk, stage_in, out_sc, out_id, out_cnt, tmp;
+
+  bool prof = false;
+  struct Pending {
+    int fam;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  double ms[K_NFAM] = {0};
+  int64_t launches[K_NFAM] = {0};
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Run a launcher with optional event bracketing for the profiler.
+template <typename F>
+int timed(bb_index* x, int fam, hipStream_t s, F&& launch) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (x->prof) {
+    BB_HIP(hipEventCreate(&a));
+    BB_HIP(hipEventCreate(&b));
+    BB_HIP(hipEventRecord(a, s));
+  }
+  hipError_t e = launch();
+  if (e != hipSuccess) {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    return fail(BB_E_HIP, std::string("launch ") + kFamNames[fam] + ": " + hipGetErrorString(e));
+  }
+  if (x->prof) {
+    BB_HIP(hipEventRecord(b, s));
+    x->pending.push_back({fam, a, b});
+    x->launches[fam] += 1;
+  }
+  return BB_OK;
+}
+
+// Copy `bytes` of a caller buffer to the device when it is a host pointer; returns the
+// device-side pointer to use.
+int to_device(bb_index* x, DevBuf& buf, size_t off, const void* src, size_t bytes, int where, hipStream_t s,
+              const void** out) {
+  if (!src || bytes == 0) {
+    *out = src;
+    return BB_OK;
+  }
+  if (where == BB_DEVICE) {
+    *out = src;
+    return BB_OK;
+  }
+  BB_HIP(hipMemcpyAsync((char*)buf.p + off, src, bytes, hipMemcpyHostToDevice, s));
+  *out = (char*)buf.p + off;
+  return BB_OK;
+}
+
+int side_k_int(const bb_query* q, int32_t* sides, int32_t* k_int) {
+  if (!q) return fail(BB_E_ARG, "null query");
+  if (q->k <= 0) return fail(BB_E_ARG, "k must be > 0");
+  const int ks = q->k_side > 0 ? q->k_side : 2 * q->k;
+  switch (q->mode) {
+    case BB_MODE_SEMANTIC:
+    case BB_MODE_CF:
+      *sides = 1;
+      *k_int = q->k;
+      break;
+    case BB_MODE_SIMILAR:
+      *sides = 1;
+      *k_int = q->k + 1;
+      break;
+    case BB_MODE_HYBRID:
+      *sides = 2;
+      *k_int = ks + 1;
+      break;
+    default:
+      return fail(BB_E_ARG, "unknown mode " + std::to_string(q->mode));
+  }
+  if (*k_int > kMaxKInt) return fail(BB_E_ARG, "k too large (internal list " + std::to_string(*k_int) +
+                                                    " > " + std::to_string(kMaxKInt) + ")");
+  return BB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* bb_last_error(void) { return g_err.c_str(); }
+int bb_abi_version(void) { return BB_ABI_VERSION; }
+
+int bb_create(const bb_desc* desc, bb_index** out) {
+  if (!out) return fail(BB_E_ARG, "null out");
+  *out = nullptr;
+  int dev = desc ? desc->device : -1;
+  if (dev < 0) BB_HIP(hipGetDevice(&dev));
+  int ndev = 0;
+  BB_HIP(hipGetDeviceCount(&ndev));
+  if (dev >= ndev) return fail(BB_E_ARG, "device " + std::to_string(dev) + " out of range");
+  const int dtype = desc ? desc->dtype : F32;
+  if (dtype != F32 && dtype != BF16) return fail(BB_E_ARG, "index dtype must be BB_F32 or BB_BF16");
+  DeviceGuard g(dev);
+  bb_index* x = new bb_index();
+  x->device = dev;
+  x->dtype = dtype;
+  x->id_offset = desc ? desc->id_offset : 0;
+  if (desc && desc->workspace_bytes > 0) x->ws_cap = desc->workspace_bytes;
+  hipError_t e = hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete x;
+    return fail(BB_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  *out = x;
+  return BB_OK;
+}
+
+int bb_destroy(bb_index* x) {
+  if (!x) return BB_OK;
+  {
+    DeviceGuard g(x->device);
+    (void)hipStreamSynchronize(x->stream);
+    for (auto& p : x->pending) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    for (DevBuf* b : {&x->items, &x->items_present, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S,
+                      &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp})
+      b->release();
+    (void)hipStreamDestroy(x->stream);
+  }
+  delete x;
+  return BB_OK;
+}
+
+int bb_info(bb_index* x, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* r) {
+  if (!x) return fail(BB_E_ARG, "null index");
+  if (n_items) *n_items = x->n;
+  if (d) *d = x->d;
+  if (d_pad) *d_pad = x->Dpad;
+  if (r) *r = x->r;
+  return BB_OK;
+}
+
+// Upload rows (host or device) in chunks through the staging buffer and convert them into
+// dst (Npad × ldst, index dtype), normalising when asked.
+static int upload_rows(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t in_dtype, int normalize,
+                       int where, void* dst, int64_t ldst) {
+  const size_t es = elem_size(in_dtype);
+  const size_t row_bytes = (size_t)d * es;
+  const int64_t chunk = std::max<int64_t>(1, (int64_t)((256ull << 20) / row_bytes));
+  if (where == BB_HOST) {
+    int rc = x->tmp.ensure(std::min<int64_t>(chunk, n) * row_bytes);
+    if (rc) return rc;
+  }
+  for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+    const int64_t nr = std::min(chunk, n - r0);
+    const void* src = (const char*)rows + (size_t)r0 * row_bytes;
+    if (where == BB_HOST) {
+      BB_HIP(hipMemcpyAsync(x->tmp.p, src, nr * row_bytes, hipMemcpyHostToDevice, x->stream));
+      src = x->tmp.p;
+    }
+    char* d0 = (char*)dst + (size_t)r0 * ldst * elem_size(x->dtype);
+    BB_HIP(launch_convert_rows(src, in_dtype, nr, d, normalize, d0, x->dtype, ldst, x->stream));
+  }
+  BB_HIP(hipStreamSynchronize(x->stream));
+  return BB_OK;
+}
+
+int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t in_dtype, int32_t prenormalized,
+                    int32_t where, const uint32_t* present_bits) {
+  if (!x || !rows || n <= 0 || d <= 0) return fail(BB_E_ARG, "bb_upload_items: bad arguments");
+  if (in_dtype != F32 && in_dtype != BF16 && in_dtype != F64) return fail(BB_E_ARG, "bad input dtype");
+  if (n >= 0xFFFFFFFFll - x->id_offset) return fail(BB_E_ARG, "too many items for 32-bit ids");
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  x->n = n;
+  x->d = d;
+  x->Npad = round_up(n, kTileRows);
+  x->Dpad = (int)round_up(d, gemm_tile_k(x->dtype));
+  const size_t bytes = (size_t)x->Npad * x->Dpad * elem_size(x->dtype);
+  int rc = x->items.ensure(bytes);
+  if (rc) return rc;
+  BB_HIP(hipMemsetAsync(x->items.p, 0, bytes, x->stream));
+  const size_t wbytes = (size_t)(x->Npad / 32) * 4;
+  if ((rc = x->items_present.ensure(wbytes))) return rc;
+  if (present_bits) {
+    BB_HIP(hipMemsetAsync(x->items_present.p, 0, wbytes, x->stream));
+    BB_HIP(hipMemcpyAsync(x->items_present.p, present_bits, (size_t)((n + 31) / 32) * 4, hipMemcpyHostToDevice,
+                          x->stream));
+  } else {
+    BB_HIP(hipMemsetAsync(x->items_present.p, 0xFF, wbytes, x->stream));
+  }
+  return upload_rows(x, rows, n, d, in_dtype, prenormalized ? 0 : 1, where, x->items.p, x->Dpad);
+}
+
+int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const uint32_t* present_bits) {
+  if (!x || !f || r <= 0) return fail(BB_E_ARG, "bb_upload_cf: bad arguments");
+  if (x->n <= 0) return fail(BB_E_STATE, "upload items before CF factors");
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  x->r = r;
+  x->Rpad = (int)round_up(r, gemm_tile_k(x->dtype));
+  const size_t bytes = (size_t)x->Npad * x->Rpad * elem_size(x->dtype);
+  int rc = x->cf.ensure(bytes);
+  if (rc) return rc;
+  BB_HIP(hipMemsetAsync(x->cf.p, 0, bytes, x->stream));
+  const size_t wbytes = (size_t)(x->Npad / 32) * 4;
+  if ((rc = x->cf_present.ensure(wbytes))) return rc;
+  if (present_bits) {
+    BB_HIP(hipMemsetAsync(x->cf_present.p, 0, wbytes, x->stream));
+    BB_HIP(hipMemcpyAsync(x->cf_present.p, present_bits, (size_t)((x->n + 31) / 32) * 4, hipMemcpyHostToDevice,
+                          x->stream));
+  } else {
+    BB_HIP(hipMemsetAsync(x->cf_present.p, 0xFF, wbytes, x->stream));
+  }
+  return upload_rows(x, f, x->n, r, in_dtype, 0, BB_HOST, x->cf.p, x->Rpad);
+}
+
+int bb_upload_attrs(bb_index* x, const int32_t* num_parts, const int16_t* year, const int32_t* theme_id) {
+  if (!x || !num_parts || !year || !theme_id) return fail(BB_E_ARG, "bb_upload_attrs: bad arguments");
+  if (x->n <= 0) return fail(BB_E_STATE, "upload items before attributes");
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  int rc;
+  if ((rc = x->parts.ensure(x->n * 4)) || (rc = x->year.ensure(x->n * 2)) || (rc = x->theme.ensure(x->n * 4)))
+    return rc;
+  BB_HIP(hipMemcpyAsync(x->parts.p, num_parts, x->n * 4, hipMemcpyHostToDevice, x->stream));
+  BB_HIP(hipMemcpyAsync(x->year.p, year, x->n * 2, hipMemcpyHostToDevice, x->stream));
+  BB_HIP(hipMemcpyAsync(x->theme.p, theme_id, x->n * 4, hipMemcpyHostToDevice, x->stream));
+  BB_HIP(hipStreamSynchronize(x->stream));
+  return BB_OK;
+}
+
+int bb_eval_mask(bb_index* x, const bb_predicate* p, uint32_t* out_bits, int32_t where) {
+  if (!x || !p || !out_bits) return fail(BB_E_ARG, "bb_eval_mask: bad arguments");
+  if (!x->parts.p) return fail(BB_E_STATE, "upload attributes before evaluating masks");
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  const int64_t nw = (x->n + 31) / 32;
+  const size_t tb = (size_t)((std::max(p->n_theme_bits, 0) + 31) / 32) * 4;
+  const size_t ib = (size_t)std::max<int64_t>(p->n_excluded, 0) * 8;
+  int rc = x->stage_in.ensure(nw * 4 + tb + ib + 64);
+  if (rc) return rc;
+  char* base = (char*)x->stage_in.p;
+  uint32_t* dout = where == BB_DEVICE ? out_bits : (uint32_t*)base;
+  uint32_t* dtheme = (uint32_t*)(base + round_up(nw * 4, 16));
+  int64_t* dids = (int64_t*)(base + round_up(nw * 4, 16) + round_up(tb, 16));
+  if (p->theme_mode && tb && p->theme_bits)
+    BB_HIP(hipMemcpyAsync(dtheme, p->theme_bits, tb, hipMemcpyHostToDevice, x->stream));
+  MaskArgs m{};
+  m.parts = (const int32_t*)x->parts.p;
+  m.year = (const int16_t*)x->year.p;
+  m.theme = (const int32_t*)x->theme.p;
+  m.n = x->n;
+  m.parts_min = p->parts_min;
+  m.parts_max = p->parts_max;
+  m.year_min = p->year_min;
+  m.year_max = p->year_max;
+  m.theme_mode = (p->theme_mode && p->theme_bits) || p->theme_mode == 1 ? p->theme_mode : 0;
+  m.n_theme_bits = p->theme_bits ? p->n_theme_bits : 0;
+  m.theme_bits = dtheme;
+  m.out = dout;
+  if ((rc = timed(x, K_MASK, x->stream, [&] { return launch_mask(m, x->stream); }))) return rc;
+  if (p->n_excluded > 0 && p->excluded_items) {
+    std::vector<int64_t> local(p->n_excluded);
+    for (int64_t i = 0; i < p->n_excluded; ++i) local[i] = p->excluded_items[i] - x->id_offset;
+    BB_HIP(hipMemcpyAsync(dids, local.data(), ib, hipMemcpyHostToDevice, x->stream));
+    BB_HIP(launch_clear_bits(dout, dids, p->n_excluded, x->n, x->stream));
+    BB_HIP(hipStreamSynchronize(x->stream));  // `local` goes out of scope
+  }
+  if (where != BB_DEVICE) {
+    BB_HIP(hipMemcpyAsync(out_bits, dout, nw * 4, hipMemcpyDeviceToHost, x->stream));
+  }
+  BB_HIP(hipStreamSynchronize(x->stream));
+  return BB_OK;
+}
+
+int bb_key_lens(const bb_query* q, int32_t* sides, int32_t* k_int) { return side_k_int(q, sides, k_int); }
+
+int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
+  if (!x || !q || !res) return fail(BB_E_ARG, "null argument");
+  int32_t sides, K_int;
+  int rc = side_k_int(q, &sides, &K_int);
+  if (rc) return rc;
+  const int B = q->B;
+  if (B <= 0) return fail(BB_E_ARG, "B must be > 0");
+  if (x->n <= 0) return fail(BB_E_STATE, "no items uploaded");
+  const bool need_content = q->mode != BB_MODE_CF;
+  const bool need_cf = q->mode == BB_MODE_CF || q->mode == BB_MODE_HYBRID;
+  const bool drop = q->mode == BB_MODE_SIMILAR || q->mode == BB_MODE_HYBRID;
+  if (need_cf && !x->cf.p) return fail(BB_E_STATE, "CF mode needs bb_upload_cf");
+  if (need_content && q->mode != BB_MODE_SEMANTIC && !q->q_items && !q->q_rows)
+    return fail(BB_E_ARG, "similar/hybrid mode needs q_items (or pre-normalised q_rows)");
+  if (q->mode == BB_MODE_SEMANTIC && !q->q_rows) return fail(BB_E_ARG, "semantic mode needs q_rows");
+  if (need_cf && !q->q_cf) return fail(BB_E_ARG, "cf/hybrid mode needs q_cf");
+  const bool out_keys = (q->flags & BB_Q_OUT_KEYS) != 0;
+  if (out_keys && (!res->keys || !res->max_keys)) return fail(BB_E_ARG, "BB_Q_OUT_KEYS needs keys/max_keys");
+  if (!out_keys && (!res->scores || !res->ids)) return fail(BB_E_ARG, "null result buffers");
+
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  hipStream_t s = (q->flags & BB_Q_NULL_STREAM) ? (hipStream_t)0 : q->stream ? (hipStream_t)q->stream : x->stream;
+  const int where = q->where;
+  const int64_t nw = (x->n + 31) / 32;
+
+  // slab / chunk geometry
+  const int64_t slab = std::min<int64_t>(x->Npad, (int64_t)kSelectStageMax);
+  const int64_t n_slabs = (x->n + slab - 1) / slab;
+  const int64_t lds = slab;  // multiple of kTileRows
+  int64_t Bc = std::max<int64_t>(kTileRows, (x->ws_cap / (lds * 4)) / kTileRows * kTileRows);
+  Bc = std::min<int64_t>(Bc, round_up(B, kTileRows));
+
+  // stage host inputs
+  const size_t es_q = elem_size(q->q_dtype), es_cf = elem_size(q->q_cf_dtype);
+  const size_t b_rows = q->q_rows ? (size_t)B * x->d * es_q : 0;
+  const size_t b_items = q->q_items ? (size_t)B * 8 : 0;
+  const size_t b_cf = q->q_cf && need_cf ? (size_t)B * x->r * es_cf : 0;
+  const size_t b_mask = q->mask_bits ? (size_t)nw * 4 : 0;
+  const size_t b_excl = q->excl_bits ? (size_t)B * nw * 4 : 0;
+  size_t off_rows = 0, off_items = round_up(b_rows, 256), off_cf = off_items + round_up(b_items, 256),
+         off_mask = off_cf + round_up(b_cf, 256), off_excl = off_mask + round_up(b_mask, 256),
+         stage_total = off_excl + round_up(b_excl, 256);
+  if (where == BB_HOST && (rc = x->stage_in.ensure(std::max<size_t>(stage_total, 256)))) return rc;
+  const void *d_rows, *d_items, *d_cf, *d_mask, *d_excl;
+  if ((rc = to_device(x, x->stage_in, off_rows, q->q_rows, b_rows, where, s, &d_rows)) ||
+      (rc = to_device(x, x->stage_in, off_items, q->q_items, b_items, where, s, &d_items)) ||
+      (rc = to_device(x, x->stage_in, off_cf, q->q_cf, b_cf, where, s, &d_cf)) ||
+      (rc = to_device(x, x->stage_in, off_mask, q->mask_bits, b_mask, where, s, &d_mask)) ||
+      (rc = to_device(x, x->stage_in, off_excl, q->excl_bits, b_excl, where, s, &d_excl)))
+    return rc;
+
+  // workspace
+  const size_t es = elem_size(x->dtype);
+  if ((rc = x->S.ensure((size_t)Bc * lds * 4))) return rc;
+  if (need_content && (rc = x->qn.ensure((size_t)Bc * x->Dpad * es))) return rc;
+  if (need_cf && (rc = x->qcf.ensure((size_t)Bc * x->Rpad * es))) return rc;
+  const size_t side_keys = (size_t)Bc * K_int;
+  if ((rc = x->keys.ensure(2 * sides * side_keys * 8))) return rc;
+  if ((rc = x->maxk.ensure((size_t)Bc * 8))) return rc;
+  const bool host_out = !out_keys && res->where != BB_DEVICE;
+  if (host_out) {
+    if ((rc = x->out_sc.ensure((size_t)B * q->k * 4)) || (rc = x->out_id.ensure((size_t)B * q->k * 8)) ||
+        (rc = x->out_cnt.ensure((size_t)B * 4)))
+      return rc;
+  }
+  float* o_sc = host_out ? (float*)x->out_sc.p : res->scores;
+  int64_t* o_id = host_out ? (int64_t*)x->out_id.p : res->ids;
+  int32_t* o_cnt = host_out ? (int32_t*)x->out_cnt.p : res->counts;
+  uint64_t* keys = (uint64_t*)x->keys.p;
+  uint64_t* maxk = (uint64_t*)x->maxk.p;
+
+  for (int64_t b0 = 0; b0 < B; b0 += Bc) {
+    const int bc = (int)std::min<int64_t>(Bc, B - b0);
+    const int bpad = (int)round_up(bc, kTileRows);
+    // ---- query prep ----
+    if (need_content) {
+      PrepArgs pa{};
+      pa.Bpad = bpad;
+      pa.B = bc;
+      pa.d = x->d;
+      pa.Dpad = x->Dpad;
+      pa.out = x->qn.p;
+      pa.out_dtype = x->dtype;
+      pa.items = x->items.p;
+      pa.n_items = x->n;
+      pa.id_offset = x->id_offset;
+      if (q->mode != BB_MODE_SEMANTIC && d_items) {
+        pa.item_ids = (const int64_t*)d_items + b0;
+      } else {
+        pa.src = (const char*)d_rows + (size_t)b0 * x->d * es_q;
+        pa.src_dtype = q->q_dtype;
+        pa.src_ld = x->d;
+        pa.normalize = q->mode == BB_MODE_SEMANTIC ? 1 : 0;
+      }
+      if ((rc = timed(x, K_PREP, s, [&] { return launch_prep(pa, s); }))) return rc;
+    }
+    if (need_cf) {
+      PrepArgs pa{};
+      pa.Bpad = bpad;
+      pa.B = bc;
+      pa.d = x->r;
+      pa.Dpad = x->Rpad;
+      pa.out = x->qcf.p;
+      pa.out_dtype = x->dtype;
+      pa.src = (const char*)d_cf + (size_t)b0 * x->r * es_cf;
+      pa.src_dtype = q->q_cf_dtype;
+      pa.src_ld = x->r;
+      pa.normalize = 0;
+      if ((rc = timed(x, K_PREP, s, [&] { return launch_prep(pa, s); }))) return rc;
+    }
+    // ---- per side: slabs of gemm + select ----
+    int final_pp = 0;
+    for (int side = 0; side < sides; ++side) {
+      const bool cf_side = (q->mode == BB_MODE_CF) || (q->mode == BB_MODE_HYBRID && side == 1);
+      const bool side_drop = drop && side == 0;
+      for (int64_t sl = 0; sl < n_slabs; ++sl) {
+        const int64_t c0 = sl * slab;
+        const int ncols = (int)std::min<int64_t>(slab, x->n - c0);
+        const int ncols_pad = (int)round_up(ncols, kTileRows);
+        GemmArgs ga{};
+        ga.Q = cf_side ? x->qcf.p : x->qn.p;
+        ga.ldq = cf_side ? x->Rpad : x->Dpad;
+        ga.X = (const char*)(cf_side ? x->cf.p : x->items.p) + (size_t)c0 * ga.ldq * es;
+        ga.ldx = ga.ldq;
+        ga.S = (float*)x->S.p;
+        ga.lds = lds;
+        ga.Mpad = bpad;
+        ga.Ncols = ncols_pad;
+        ga.Kpad = (int)ga.ldq;
+        if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(x->dtype, ga, s); }))) return rc;
+        const int pp = (int)(sl & 1);
+        SelectArgs sa{};
+        sa.S = (const float*)x->S.p;
+        sa.lds = lds;
+        sa.n_cols = ncols;
+        sa.slab_start = c0;
+        sa.gid0 = (uint32_t)(x->id_offset + c0);
+        sa.mask = (const uint32_t*)d_mask;
+        sa.present = (const uint32_t*)(cf_side ? x->cf_present.p : x->items_present.p);
+        sa.excl = cf_side && d_excl ? (const uint32_t*)d_excl + (size_t)b0 * nw : nullptr;
+        sa.excl_ld = nw;
+        sa.K = K_int;
+        sa.carry_in = sl ? keys + ((size_t)(pp ^ 1) * sides + side) * side_keys : nullptr;
+        sa.keys_out = keys + ((size_t)pp * sides + side) * side_keys;
+        sa.max_inout = side_drop ? maxk : nullptr;
+        sa.first_slab = sl == 0;
+        if ((rc = timed(x, K_SELECT, s, [&] { return launch_select(sa, bc, s); }))) return rc;
+        final_pp = pp;
+      }
+    }
+    const uint64_t* fin_keys = keys + (size_t)final_pp * sides * side_keys;
+    if (out_keys) {
+      for (int side = 0; side < sides; ++side)
+        BB_HIP(hipMemcpyAsync(res->keys + ((size_t)side * B + b0) * K_int, fin_keys + (size_t)side * side_keys,
+                              (size_t)bc * K_int * 8, hipMemcpyDeviceToDevice, s));
+      if (drop)
+        BB_HIP(hipMemcpyAsync(res->max_keys + b0, maxk, (size_t)bc * 8, hipMemcpyDeviceToDevice, s));
+      else
+        BB_HIP(hipMemsetAsync(res->max_keys + b0, 0, (size_t)bc * 8, s));
+      continue;
+    }
+    FinalizeArgs fa{};
+    fa.keys = fin_keys;
+    fa.max_keys = drop ? maxk : nullptr;
+    fa.P = 1;
+    fa.sides = sides;
+    fa.B = (int)Bc;  // row stride of the per-side key blocks
+    fa.K_int = K_int;
+    fa.drop_rank0 = drop;
+    fa.k = q->k;
+    fa.k_side = q->k_side > 0 ? q->k_side : 2 * q->k;
+    fa.hybrid = q->mode == BB_MODE_HYBRID;
+    fa.w_content = q->w_content;
+    fa.w_cf = q->w_cf;
+    fa.scores = o_sc + (size_t)b0 * q->k;
+    fa.ids = o_id + (size_t)b0 * q->k;
+    fa.counts = o_cnt ? o_cnt + b0 : nullptr;
+    fa.n_rows = bc;
+    if ((rc = timed(x, K_FIN, s, [&] { return launch_finalize(fa, s); }))) return rc;
+  }
+  if (host_out) {
+    BB_HIP(hipMemcpyAsync(res->scores, o_sc, (size_t)B * q->k * 4, hipMemcpyDeviceToHost, s));
+    BB_HIP(hipMemcpyAsync(res->ids, o_id, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
+    if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, o_cnt, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+  }
+  if (host_out || where == BB_HOST) BB_HIP(hipStreamSynchronize(s));
+  return BB_OK;
+}
+
+int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint64_t* max_keys, int32_t n_parts,
+                bb_result* res) {
+  if (!x || !q || !keys || !res || n_parts <= 0) return fail(BB_E_ARG, "bb_finalize: bad arguments");
+  int32_t sides, K_int;
+  int rc = side_k_int(q, &sides, &K_int);
+  if (rc) return rc;
+  if (n_parts * K_int > 4096) return fail(BB_E_ARG, "bb_finalize: n_parts * k_int > 4096");
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  hipStream_t s = (q->flags & BB_Q_NULL_STREAM) ? (hipStream_t)0 : q->stream ? (hipStream_t)q->stream : x->stream;
+  const int B = q->B;
+  const bool host_out = res->where != BB_DEVICE;
+  if (host_out) {
+    if ((rc = x->out_sc.ensure((size_t)B * q->k * 4)) || (rc = x->out_id.ensure((size_t)B * q->k * 8)) ||
+        (rc = x->out_cnt.ensure((size_t)B * 4)))
+      return rc;
+  }
+  const bool drop = q->mode == BB_MODE_SIMILAR || q->mode == BB_MODE_HYBRID;
+  FinalizeArgs fa{};
+  fa.keys = keys;
+  fa.max_keys = drop ? max_keys : nullptr;
+  fa.P = n_parts;
+  fa.sides = sides;
+  fa.B = B;
+  fa.K_int = K_int;
+  fa.drop_rank0 = drop;
+  fa.k = q->k;
+  fa.k_side = q->k_side > 0 ? q->k_side : 2 * q->k;
+  fa.hybrid = q->mode == BB_MODE_HYBRID;
+  fa.w_content = q->w_content;
+  fa.w_cf = q->w_cf;
+  fa.scores = host_out ? (float*)x->out_sc.p : res->scores;
+  fa.ids = host_out ? (int64_t*)x->out_id.p : res->ids;
+  fa.counts = host_out ? (int32_t*)x->out_cnt.p : res->counts;
+  fa.n_rows = B;
+  if ((rc = timed(x, K_FIN, s, [&] { return launch_finalize(fa, s); }))) return rc;
+  if (host_out) {
+    BB_HIP(hipMemcpyAsync(res->scores, x->out_sc.p, (size_t)B * q->k * 4, hipMemcpyDeviceToHost, s));
+    BB_HIP(hipMemcpyAsync(res->ids, x->out_id.p, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
+    if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, x->out_cnt.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+    BB_HIP(hipStreamSynchronize(s));
+  }
+  return BB_OK;
+}
+
+int bb_set_profiling(bb_index* x, int32_t on) {
+  if (!x) return fail(BB_E_ARG, "null index");
+  x->prof = on != 0;
+  return BB_OK;
+}
+
+int bb_get_profile(bb_index* x, bb_profile* out) {
+  if (!x || !out) return fail(BB_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  for (auto& p : x->pending) {
+    BB_HIP(hipEventSynchronize(p.b));
+    float ms = 0.f;
+    BB_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    x->ms[p.fam] += ms;
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  x->pending.clear();
+  std::memset(out, 0, sizeof(*out));
+  out->n = K_NFAM;
+  for (int i = 0; i < K_NFAM; ++i) {
+    out->ms[i] = x->ms[i];
+    out->launches[i] = x->launches[i];
+    out->names[i] = kFamNames[i];
+    x->ms[i] = 0;
+    x->launches[i] = 0;
+  }
+  return BB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,117 @@
+// common.h — shared device/host definitions of libbrickrec (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bb {
+
+// ---- item ordering keys ------------------------------------------------------------------
+// A candidate is one u64: high word = order-preserving image of the fp32 score, low word =
+// 0xFFFFFFFF - global id.  "larger key" == (score desc, id asc), the fixed tie rule of
+// SURVEY.md §8a(v).  Key 0 (ord 0 = the image of -NaN 0xFFFFFFFF) marks an empty slot;
+// every non-NaN float maps to ord >= 0x007FFFFF, so real candidates are never 0.
+__host__ __device__ inline uint32_t ord_of(float f) {
+  uint32_t u = __builtin_bit_cast(uint32_t, f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float float_of_ord(uint32_t o) {
+  uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+  return __builtin_bit_cast(float, u);
+}
+__host__ __device__ inline uint64_t make_key(uint32_t ord, uint32_t gid) {
+  return ((uint64_t)ord << 32) | (uint32_t)(0xFFFFFFFFu - gid);
+}
+__host__ __device__ inline uint32_t gid_of(uint64_t key) { return 0xFFFFFFFFu - (uint32_t)key; }
+__host__ __device__ inline uint32_t ordk_of(uint64_t key) { return (uint32_t)(key >> 32); }
+
+// ---- tiling constants ---------------------------------------------------------------------
+constexpr int kTileRows = 128;     // item / query rows are padded to this multiple
+constexpr int kSelectThreads = 256;
+constexpr int kSelectStageMax = 32768;  // score row staged in LDS when n_cols <= this
+constexpr int kMaxKInt = 512;      // per-side internal list length limit (k_side + 1)
+
+enum Dtype : int { F32 = 0, BF16 = 1, F64 = 2 };
+
+struct GemmArgs {
+  const void* Q;      // [Mpad][ldq]   queries (normalised), dtype of the index
+  const void* X;      // [Npad][ldx]   item rows of the slab (row 0 = slab start)
+  float* S;           // [Mpad][lds]   scores out
+  int64_t ldq, ldx, lds;
+  int32_t Mpad;       // multiple of the block-tile M
+  int32_t Ncols;      // multiple of the block-tile N
+  int32_t Kpad;       // reduction length, multiple of the k-tile
+};
+
+struct SelectArgs {
+  const float* S;           // scores [B][lds]
+  int64_t lds;
+  int32_t n_cols;           // real columns in this slab
+  int64_t slab_start;       // local item index of column 0
+  uint32_t gid0;            // global id of column 0 (= id_offset + slab_start)
+  const uint32_t* mask;     // local-item bitset or null
+  const uint32_t* present;  // local-item bitset or null: the side's item space (rank-0 too)
+  const uint32_t* excl;     // per-query local-item bitset or null
+  int64_t excl_ld;          // words per query in excl
+  int32_t K;                // internal list length (<= kMaxKInt)
+  const uint64_t* carry_in; // [B][K] keys of previous slabs, or null
+  uint64_t* keys_out;       // [B][K]
+  uint64_t* max_inout;      // [B] running unmasked arg-max key, or null
+  int32_t first_slab;       // max_inout is overwritten (not merged) when set
+};
+
+struct FinalizeArgs {
+  const uint64_t* keys;     // [P][sides][B][K_int]
+  const uint64_t* max_keys; // [P][B] or null
+  int32_t P, sides, B, K_int;  // B = row stride of each [side] key block
+  int32_t n_rows;               // queries to finalize (grid size)
+  int32_t drop_rank0;       // side 0 (content / similar) drops the global arg-max
+  int32_t k;                // final length
+  int32_t k_side;           // hybrid per-side length
+  int32_t hybrid;
+  double w_content, w_cf;
+  float* scores;            // [B][k]
+  int64_t* ids;             // [B][k]
+  int32_t* counts;          // [B] or null
+};
+
+struct PrepArgs {
+  const void* src;          // query rows [B][d] (q_dtype) or null
+  int32_t src_dtype;
+  int64_t src_ld;
+  const int64_t* item_ids;  // global ids (gather from the item matrix) or null
+  int64_t id_offset;
+  const void* items;        // item matrix [Npad][Dpad] index dtype (for gathers)
+  int64_t n_items;
+  int32_t d, Dpad;          // real and padded widths
+  int32_t normalize;        // 1 = divide by L2 norm (sklearn normalize semantics)
+  void* out;                // [Bpad][Dpad] index dtype
+  int32_t out_dtype;
+  int32_t B, Bpad;
+};
+
+struct MaskArgs {
+  const int32_t* parts;
+  const int16_t* year;
+  const int32_t* theme;
+  int64_t n;
+  int32_t parts_min, parts_max, year_min, year_max;
+  int32_t theme_mode, n_theme_bits;
+  const uint32_t* theme_bits;  // device copy
+  uint32_t* out;               // [ceil(n/32)] words
+};
+
+// launchers (stream-ordered, no sync, no allocation)
+hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s);
+int gemm_tile_m(int dtype);
+int gemm_tile_n(int dtype);
+int gemm_tile_k(int dtype);
+hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s);
+hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
+hipError_t launch_prep(const PrepArgs& a, hipStream_t s);
+hipError_t launch_mask(const MaskArgs& a, hipStream_t s);
+hipError_t launch_clear_bits(uint32_t* bits, const int64_t* ids, int64_t n_ids, int64_t n_items,
+                             hipStream_t s);
+hipError_t launch_convert_rows(const void* src, int src_dtype, int64_t n, int d, int normalize,
+                               void* dst, int dst_dtype, int64_t Dpad, hipStream_t s);
+
+}  // namespace bb

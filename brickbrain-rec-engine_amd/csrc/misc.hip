@@ -1,0 +1,331 @@
+// misc.hip — query preparation, cross-slab/shard finalize (rank-0 drop, hybrid
+// union-blend), hard-constraint predicate masks and item-row conversion (gfx950).
+#include "common.h"
+
+namespace bb {
+
+__device__ __forceinline__ float load_elem(const void* p, int dtype, size_t i) {
+  if (dtype == F32) return ((const float*)p)[i];
+  if (dtype == BF16) return __builtin_bit_cast(float, (uint32_t)((const uint16_t*)p)[i] << 16);
+  return (float)((const double*)p)[i];
+}
+__device__ __forceinline__ double load_elem_d(const void* p, int dtype, size_t i) {
+  if (dtype == F64) return ((const double*)p)[i];
+  return (double)load_elem(p, dtype, i);
+}
+// round-to-nearest-even f32 -> bf16 (NaN kept NaN)
+__device__ __forceinline__ uint16_t to_bf16(float f) {
+  uint32_t u = __builtin_bit_cast(uint32_t, f);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ void store_elem(void* p, int dtype, size_t i, float v) {
+  if (dtype == BF16)
+    ((uint16_t*)p)[i] = to_bf16(v);
+  else
+    ((float*)p)[i] = v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// rows -> (optionally L2-normalised) rows of the index dtype, padded to Dpad.
+// Normalisation follows sklearn.preprocessing.normalize, which cosine_similarity applies
+// to both arguments (recommendation_system.py:214): norm = sqrt(Σx²) (accumulated in f64
+// here), zero norms -> 1, then a true division.  One wave per row.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void convert_rows_kernel(const void* src, int src_dtype, int64_t n, int d,
+                                                           int normalize, void* dst, int dst_dtype,
+                                                           int64_t Dpad) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const size_t sb = (size_t)row * d, db = (size_t)row * Dpad;
+  double norm = 1.0;
+  if (normalize) {
+    double ss = 0.0;
+    for (int i = lane; i < d; i += 64) {
+      const double x = load_elem_d(src, src_dtype, sb + i);
+      ss += x * x;
+    }
+    ss = wave_sum(ss);
+    norm = sqrt(ss);
+    if (norm == 0.0) norm = 1.0;
+  }
+  for (int i = lane; i < Dpad; i += 64) {
+    float v = 0.f;
+    if (i < d) v = (float)(load_elem_d(src, src_dtype, sb + i) / norm);
+    store_elem(dst, dst_dtype, db + i, v);
+  }
+}
+
+hipError_t launch_convert_rows(const void* src, int src_dtype, int64_t n, int d, int normalize, void* dst,
+                               int dst_dtype, int64_t Dpad, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = (n + 3) / 4;
+  hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, src_dtype, n, d,
+                     normalize, dst, dst_dtype, Dpad);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// query preparation: normalise query rows (semantic), or gather the stored (already
+// normalised) item rows of the liked sets (similar-sets: the query IS feat_matrix[target],
+// recommendation_system.py:213), or copy user factor rows (CF, :435).  Rows >= B are zero.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.Bpad) return;
+  const size_t ob = (size_t)row * a.Dpad;
+  if (row >= a.B) {
+    for (int i = lane; i < a.Dpad; i += 64) store_elem(a.out, a.out_dtype, ob + i, 0.f);
+    return;
+  }
+  if (a.item_ids) {
+    const int64_t lid = a.item_ids[row] - a.id_offset;
+    const bool ok = lid >= 0 && lid < a.n_items;
+    for (int i = lane; i < a.Dpad; i += 64) {
+      const float v = ok ? load_elem(a.items, a.out_dtype, (size_t)lid * a.Dpad + i) : 0.f;
+      store_elem(a.out, a.out_dtype, ob + i, v);
+    }
+    return;
+  }
+  const size_t sb = (size_t)row * a.src_ld;
+  double norm = 1.0;
+  if (a.normalize) {
+    double ss = 0.0;
+    for (int i = lane; i < a.d; i += 64) {
+      const double x = load_elem_d(a.src, a.src_dtype, sb + i);
+      ss += x * x;
+    }
+    ss = wave_sum(ss);
+    norm = sqrt(ss);
+    if (norm == 0.0) norm = 1.0;
+  }
+  for (int i = lane; i < a.Dpad; i += 64) {
+    float v = 0.f;
+    if (i < a.d) v = (float)(load_elem_d(a.src, a.src_dtype, sb + i) / norm);
+    store_elem(a.out, a.out_dtype, ob + i, v);
+  }
+}
+
+hipError_t launch_prep(const PrepArgs& a, hipStream_t s) {
+  if (a.Bpad <= 0) return hipSuccess;
+  hipLaunchKernelGGL(prep_kernel, dim3((a.Bpad + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// finalize: merge P shard lists per side, drop rank 0 (similar side), truncate, and for
+// the hybrid run _combine_recommendations (recommendation_system.py:789-843): union of the
+// two lists, h = wc·c + wcf·cf with a missing side = 0 (:812-818, in f64 like the Python
+// floats), sort by (h desc, id asc), top k.  One side empty -> the other side's top k
+// with its raw scores (:659-662).  One workgroup per query.
+// ---------------------------------------------------------------------------------------
+constexpr int kFinThreads = 256;
+constexpr int kFinMerge = 4096;  // P * K_int capacity
+
+__device__ __forceinline__ uint64_t ord64_of(double d) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+template <typename T, typename Better>
+__device__ void bitonic_desc(T* v, int P, Better better) {
+  for (int k = 2; k <= P; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += kFinThreads) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const T x = v[i], y = v[ixj];
+          const bool desc = (i & k) == 0;
+          if (desc ? better(y, x) : better(x, y)) {
+            v[i] = y;
+            v[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+struct Blend {
+  uint64_t h;   // order image of the f64 blended score
+  uint32_t gid;
+  uint32_t pad;
+  double hv;
+};
+
+__global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
+  __shared__ uint64_t buf[kFinMerge];
+  __shared__ uint64_t lists[2][kMaxKInt];
+  __shared__ int counts[2];
+  const int q = blockIdx.x, tid = threadIdx.x;
+
+  for (int side = 0; side < a.sides; ++side) {
+    const int m = a.P * a.K_int;
+    int P2 = 1;
+    while (P2 < m) P2 <<= 1;
+    for (int i = tid; i < P2; i += kFinThreads) {
+      uint64_t key = 0ull;
+      if (i < m) {
+        const int p = i / a.K_int, j = i % a.K_int;
+        key = a.keys[(((size_t)p * a.sides + side) * a.B + q) * a.K_int + j];
+      }
+      buf[i] = key;
+    }
+    __syncthreads();
+    if (a.P > 1) bitonic_desc(buf, P2, [](uint64_t x, uint64_t y) { return x > y; });
+    const bool drop = side == 0 && a.drop_rank0;
+    const int target = a.hybrid ? a.k_side : a.k;
+    if (tid == 0) {
+      int start = 0;
+      if (drop && a.max_keys) {
+        uint64_t gmax = 0;
+        for (int p = 0; p < a.P; ++p) {
+          const uint64_t v = a.max_keys[(size_t)p * a.B + q];
+          gmax = v > gmax ? v : gmax;
+        }
+        if (buf[0] == gmax && gmax) start = 1;
+      }
+      int c = 0;
+      for (int i = start; i < a.K_int && c < target; ++i) {
+        if (!buf[i]) break;
+        lists[side][c++] = buf[i];
+      }
+      counts[side] = c;
+    }
+    __syncthreads();
+  }
+
+  float* sc = a.scores + (size_t)q * a.k;
+  int64_t* id = a.ids + (size_t)q * a.k;
+  if (!a.hybrid || counts[0] == 0 || counts[1] == 0) {
+    const int side = (!a.hybrid || counts[0] > 0) ? 0 : 1;
+    const int c = counts[side] < a.k ? counts[side] : a.k;
+    for (int i = tid; i < a.k; i += kFinThreads) {
+      if (i < c) {
+        sc[i] = float_of_ord(ordk_of(lists[side][i]));
+        id[i] = (int64_t)gid_of(lists[side][i]);
+      } else {
+        sc[i] = 0.f;
+        id[i] = -1;
+      }
+    }
+    if (a.counts && tid == 0) a.counts[q] = c;
+    return;
+  }
+  // hybrid union blend
+  Blend* ent = (Blend*)buf;  // 2 * kMaxKInt entries of 24 B fit in buf (32 KB)
+  const int c0 = counts[0], c1 = counts[1];
+  __shared__ int n_ent;
+  if (tid == 0) n_ent = 0;
+  __syncthreads();
+  for (int i = tid; i < c0; i += kFinThreads) {
+    const uint32_t g = gid_of(lists[0][i]);
+    const double cs = (double)float_of_ord(ordk_of(lists[0][i]));
+    double fs = 0.0;
+    for (int j = 0; j < c1; ++j)
+      if (gid_of(lists[1][j]) == g) {
+        fs = (double)float_of_ord(ordk_of(lists[1][j]));
+        break;
+      }
+    const double h = a.w_content * cs + a.w_cf * fs;
+    const int pos = atomicAdd(&n_ent, 1);
+    ent[pos] = Blend{ord64_of(h), g, 0u, h};
+  }
+  for (int j = tid; j < c1; j += kFinThreads) {
+    const uint32_t g = gid_of(lists[1][j]);
+    bool in_c = false;
+    for (int i = 0; i < c0; ++i)
+      if (gid_of(lists[0][i]) == g) {
+        in_c = true;
+        break;
+      }
+    if (in_c) continue;
+    const double h = a.w_content * 0.0 + a.w_cf * (double)float_of_ord(ordk_of(lists[1][j]));
+    const int pos = atomicAdd(&n_ent, 1);
+    ent[pos] = Blend{ord64_of(h), g, 0u, h};
+  }
+  __syncthreads();
+  const int ne = n_ent;
+  int P2 = 1;
+  while (P2 < ne) P2 <<= 1;
+  for (int i = ne + tid; i < P2; i += kFinThreads) ent[i] = Blend{0ull, 0xFFFFFFFFu, 0u, 0.0};
+  __syncthreads();
+  bitonic_desc(ent, P2, [](const Blend& x, const Blend& y) {
+    return x.h > y.h || (x.h == y.h && x.gid < y.gid);
+  });
+  const int c = ne < a.k ? ne : a.k;
+  for (int i = tid; i < a.k; i += kFinThreads) {
+    if (i < c) {
+      sc[i] = (float)ent[i].hv;
+      id[i] = (int64_t)ent[i].gid;
+    } else {
+      sc[i] = 0.f;
+      id[i] = -1;
+    }
+  }
+  if (a.counts && tid == 0) a.counts[q] = c;
+}
+
+hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
+  if (a.n_rows <= 0) return hipSuccess;
+  if (a.n_rows > a.B || a.P * a.K_int > kFinMerge || a.K_int > kMaxKInt || a.sides < 1 || a.sides > 2) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(finalize_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// hard-constraint predicates -> mask bitset (hard_constraint_filter.py:318-480).  One item
+// per lane, one 64-bit ballot per wave -> two mask words.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mask_kernel(MaskArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool ok = false;
+  if (i < a.n) {
+    const int32_t p = a.parts[i];
+    const int32_t y = a.year[i];
+    const int32_t t = a.theme[i];
+    ok = p > 0 && p >= a.parts_min && p <= a.parts_max && y >= a.year_min && y <= a.year_max;
+    if (a.theme_mode) {
+      const bool in_set = t >= 0 && t < a.n_theme_bits && ((a.theme_bits[t >> 5] >> (t & 31)) & 1u);
+      ok = ok && t >= 0 && (a.theme_mode == 1 ? in_set : !in_set);
+    }
+  }
+  const uint64_t b = __ballot(ok);
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63)) >> 5;
+  const int64_t nw = (a.n + 31) >> 5;
+  if (lane == 0 && w0 < nw) a.out[w0] = (uint32_t)b;
+  if (lane == 32 && w0 + 1 < nw) a.out[w0 + 1] = (uint32_t)(b >> 32);
+}
+
+hipError_t launch_mask(const MaskArgs& a, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mask_kernel, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+__global__ void clear_bits_kernel(uint32_t* bits, const int64_t* ids, int64_t n_ids, int64_t n_items) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_ids) return;
+  const int64_t id = ids[i];
+  if (id < 0 || id >= n_items) return;
+  atomicAnd(&bits[id >> 5], ~(1u << (id & 31)));
+}
+
+hipError_t launch_clear_bits(uint32_t* bits, const int64_t* ids, int64_t n_ids, int64_t n_items, hipStream_t s) {
+  if (n_ids <= 0) return hipSuccess;
+  hipLaunchKernelGGL(clear_bits_kernel, dim3((unsigned)((n_ids + 255) / 256)), dim3(256), 0, s, bits, ids, n_ids,
+                     n_items);
+  return hipGetLastError();
+}
+
+}  // namespace bb
