@@ -79,12 +79,13 @@ struct bb_index {
   int64_t n = 0, Npad = 0;
   int d = 0, Dpad = 0;
   DevBuf items, items_present;
+  DevBuf ones, zeros;  // all-ones / all-zeros bitsets standing in for 'no mask' / 'no exclusions'
   int r = 0, Rpad = 0;
   DevBuf cf, cf_present;
   DevBuf parts, year, theme;
 
   // workspace
-  DevBuf qn, qcf, S, keys, maxk, stage_in, out_sc, out_id, out_cnt, tmp;
+  DevBuf qn, qcf, S, tmax, keys, maxk, stage_in, out_sc, out_id, out_cnt, tmp;
 
   bool prof = false;
   struct Pending {
@@ -216,7 +217,7 @@ int bb_destroy(bb_index* x) {
       (void)hipEventDestroy(p.a);
       (void)hipEventDestroy(p.b);
     }
-    for (DevBuf* b : {&x->items, &x->items_present, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S,
+    for (DevBuf* b : {&x->items, &x->items_present, &x->ones, &x->zeros, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S, &x->tmax,
                       &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp})
       b->release();
     (void)hipStreamDestroy(x->stream);
@@ -283,6 +284,9 @@ int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t
   } else {
     BB_HIP(hipMemsetAsync(x->items_present.p, 0xFF, wbytes, x->stream));
   }
+  if ((rc = x->ones.ensure(wbytes)) || (rc = x->zeros.ensure(wbytes))) return rc;
+  BB_HIP(hipMemsetAsync(x->ones.p, 0xFF, wbytes, x->stream));
+  BB_HIP(hipMemsetAsync(x->zeros.p, 0, wbytes, x->stream));
   return upload_rows(x, rows, n, d, in_dtype, prenormalized ? 0 : 1, where, x->items.p, x->Dpad);
 }
 
@@ -397,9 +401,14 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   const int64_t nw = (x->n + 31) / 32;
 
   // slab / chunk geometry
-  const int64_t slab = std::min<int64_t>(x->Npad, (int64_t)kSelectStageMax);
+  // A slab is as many item columns as the score workspace holds for a query chunk of up to
+  // 1024 queries; queries beyond the chunk loop over the same slabs again.
+  const int64_t Bt = std::min<int64_t>(round_up(B, kTileRows), 1024);
+  const int64_t slab = std::min<int64_t>(
+      x->Npad, std::max<int64_t>(kTileRows, (x->ws_cap / (Bt * 4)) / kTileRows * kTileRows));
   const int64_t n_slabs = (x->n + slab - 1) / slab;
-  const int64_t lds = slab;  // multiple of kTileRows
+  const int64_t lds = slab;        // multiple of kTileRows
+  const int64_t ldt = slab / 32;   // per-tile maxima per query row
   int64_t Bc = std::max<int64_t>(kTileRows, (x->ws_cap / (lds * 4)) / kTileRows * kTileRows);
   Bc = std::min<int64_t>(Bc, round_up(B, kTileRows));
 
@@ -425,6 +434,7 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   // workspace
   const size_t es = elem_size(x->dtype);
   if ((rc = x->S.ensure((size_t)Bc * lds * 4))) return rc;
+  if ((rc = x->tmax.ensure((size_t)Bc * ldt * 4 * 2))) return rc;  // tmax + pmax
   if (need_content && (rc = x->qn.ensure((size_t)Bc * x->Dpad * es))) return rc;
   if (need_cf && (rc = x->qcf.ensure((size_t)Bc * x->Rpad * es))) return rc;
   const size_t side_keys = (size_t)Bc * K_int;
@@ -441,6 +451,8 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   int32_t* o_cnt = host_out ? (int32_t*)x->out_cnt.p : res->counts;
   uint64_t* keys = (uint64_t*)x->keys.p;
   uint64_t* maxk = (uint64_t*)x->maxk.p;
+  // single-list modes (semantic / similar / CF) finish inside the last select launch
+  const bool fuse_final = !out_keys && sides == 1;
 
   for (int64_t b0 = 0; b0 < B; b0 += Bc) {
     const int bc = (int)std::min<int64_t>(Bc, B - b0);
@@ -500,11 +512,26 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
         ga.Mpad = bpad;
         ga.Ncols = ncols_pad;
         ga.Kpad = (int)ga.ldq;
+        ga.M_valid = bc;
+        ga.n_valid = ncols;
+        ga.slab_start = c0;
+        // the scan epilogue is branch-free: every bitset pointer is valid
+        const bool has_excl = cf_side && d_excl;
+        ga.mask = d_mask ? (const uint32_t*)d_mask : (const uint32_t*)x->ones.p;
+        ga.present = (const uint32_t*)(cf_side ? x->cf_present.p : x->items_present.p);
+        ga.excl = has_excl ? (const uint32_t*)d_excl + (size_t)b0 * nw : (const uint32_t*)x->zeros.p;
+        ga.excl_ld = has_excl ? nw : 0;
+        ga.tmax = (uint32_t*)x->tmax.p;
+        ga.pmax = (uint32_t*)x->tmax.p + (size_t)Bc * ldt;
+        ga.ldt = ldt;
         if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(x->dtype, ga, s); }))) return rc;
         const int pp = (int)(sl & 1);
         SelectArgs sa{};
         sa.S = (const float*)x->S.p;
         sa.lds = lds;
+        sa.tmax = ga.tmax;
+        sa.pmax = side_drop ? ga.pmax : nullptr;
+        sa.ldt = ldt;
         sa.n_cols = ncols;
         sa.slab_start = c0;
         sa.gid0 = (uint32_t)(x->id_offset + c0);
@@ -517,10 +544,17 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
         sa.keys_out = keys + ((size_t)pp * sides + side) * side_keys;
         sa.max_inout = side_drop ? maxk : nullptr;
         sa.first_slab = sl == 0;
+        if (fuse_final && sl == n_slabs - 1) {  // single-list mode: select writes the results
+          sa.out_scores = o_sc + (size_t)b0 * q->k;
+          sa.out_ids = o_id + (size_t)b0 * q->k;
+          sa.out_counts = o_cnt ? o_cnt + b0 : nullptr;
+          sa.k_final = q->k;
+        }
         if ((rc = timed(x, K_SELECT, s, [&] { return launch_select(sa, bc, s); }))) return rc;
         final_pp = pp;
       }
     }
+    if (fuse_final) continue;
     const uint64_t* fin_keys = keys + (size_t)final_pp * sides * side_keys;
     if (out_keys) {
       for (int side = 0; side < sides; ++side)

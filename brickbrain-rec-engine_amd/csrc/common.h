@@ -37,14 +37,28 @@ struct GemmArgs {
   const void* X;      // [Npad][ldx]   item rows of the slab (row 0 = slab start)
   float* S;           // [Mpad][lds]   scores out
   int64_t ldq, ldx, lds;
-  int32_t Mpad;       // multiple of the block-tile M
-  int32_t Ncols;      // multiple of the block-tile N
+  int32_t Mpad;       // multiple of the query block tile
+  int32_t Ncols;      // multiple of the item block tile
   int32_t Kpad;       // reduction length, multiple of the k-tile
+  // fused selection-bound epilogue (tmax == null disables it)
+  int32_t M_valid;          // real queries (rows >= M_valid have no exclusion row)
+  int32_t n_valid;          // real items in the slab
+  int64_t slab_start;       // local item index of slab column 0 (multiple of 32)
+  const uint32_t* mask;     // local-item bitsets (null = all)
+  const uint32_t* present;
+  const uint32_t* excl;     // per-query bitsets [M_valid][excl_ld]
+  int64_t excl_ld;
+  uint32_t* tmax;           // [Mpad][ldt] eligible max order-image per 32-item tile
+  uint32_t* pmax;           // [Mpad][ldt] present max order-image (rank-0 search) or null
+  int64_t ldt;
 };
 
 struct SelectArgs {
   const float* S;           // scores [B][lds]
   int64_t lds;
+  const uint32_t* tmax;     // [B][ldt] per-tile eligible maxima from the GEMM epilogue
+  const uint32_t* pmax;     // [B][ldt] per-tile present maxima (rank 0) or null
+  int64_t ldt;
   int32_t n_cols;           // real columns in this slab
   int64_t slab_start;       // local item index of column 0
   uint32_t gid0;            // global id of column 0 (= id_offset + slab_start)
@@ -57,6 +71,11 @@ struct SelectArgs {
   uint64_t* keys_out;       // [B][K]
   uint64_t* max_inout;      // [B] running unmasked arg-max key, or null
   int32_t first_slab;       // max_inout is overwritten (not merged) when set
+  // final output of single-list modes on the last slab (out_scores == null: keys_out)
+  float* out_scores;        // [B][k_final]
+  int64_t* out_ids;         // [B][k_final]
+  int32_t* out_counts;      // [B] or null
+  int32_t k_final;
 };
 
 struct FinalizeArgs {

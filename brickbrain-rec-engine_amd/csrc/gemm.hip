@@ -1,56 +1,96 @@
-// gemm.hip — S = Q̂ · X̂ᵀ score slabs on MFMA (gfx950).
+// gemm.hip — S = Q̂ · X̂ᵀ score slabs on MFMA (gfx950), with the selection bound fused in.
 //
 // The dense contraction behind every scoring mode: sklearn cosine_similarity's
 // safe_sparse_dot(X̂, Ŷᵀ) (recommendation_system.py:214), the CF np.dot(u, Fᵀ) (:438) and
 // pgvector's sequential-scan dot products (lego_nlp_recommeder.py:1394).  Both operands are
 // row-major with the reduction dimension contiguous ("NT"), rows padded with zeros.
 //
-// Structure: one workgroup = WM×WN waves, each wave owns SM×SN 32×32 output tiles.
-// Operands are staged global -> registers -> LDS (double buffer, one barrier per k-tile;
-// the next tile's global loads are issued before the MFMAs of the current one).  A k-tile is
-// 128 bytes of every row (32 f32 / 64 bf16); LDS rows are padded to 144 B so the 16-B
-// fragment reads (ds_read_b128) of 16 rows hit 16 distinct bank slots.
+// Structure (gemm_kernel.h): one workgroup = WM×WN waves, each wave owns SM×SN 32×32
+// output tiles.  Operands are staged global -> registers -> LDS (double buffer, one barrier
+// per k-tile; the next tile's global loads are issued before the MFMAs of the current one).
+// A k-tile is 128 bytes of every row (32 f32 / 64 bf16); LDS rows are padded to 144 B so
+// the 16-B fragment reads (ds_read_b128) of 16 rows hit 16 distinct bank slots.
 //
 // Fragment mapping.  The MFMA reduction index may be permuted freely as long as A and B
 // use the same permutation, so lane half h reads the contiguous 16-B chunk 2u+h of its row:
 //   f32  v_mfma_f32_32x32x2_f32 : one chunk = 4 k-steps (element c of lane half h is
 //                                 d = 8u + 4h + c), exact f32 fmaf chain
 //   bf16 v_mfma_f32_32x32x16_bf16: one chunk = one MFMA (k = 8h + j), f32 accumulate
-// Accumulator C/D layout (gfx950): col = lane & 31, row = (g&3) + 8(g>>2) + 4(lane>>5).
-// A = queries (rows of S), B = items (columns of S): each epilogue store of a register is
-// 32 consecutive item scores of one query row (128-B segments).
+// A = items, B = queries: accumulator register g of lane l is item (g&3)+8(g>>2)+4(l>>5)
+// of query l&31, so the epilogue stores 16-B row segments of S and reduces each query's
+// per-32-item-tile maximum over eligible items with one cross-half swap.  Those maxima let
+// the select kernel bound the K-th score from ~N/32 values and read only the ~K tiles that
+// can hold a top-K member (select.hip).
+#include <cstdlib>
+
 #include "gemm_kernel.h"
+#include "scan_kernel.h"
 
 namespace bb {
 
-// production tile configurations
+// production tile configurations: WM×WN waves, SM×SN 32×32 tiles per wave
 struct CfgF32 {
-  static constexpr int WM = 2, WN = 2, SM = 1, SN = 1;  // 64 x 64 block tile
+  static constexpr int WM = 2, WN = 2, SM = 1, SN = 1;  // 64 items × 64 queries
 };
 struct CfgBF16 {
-  static constexpr int WM = 2, WN = 2, SM = 2, SN = 2;  // 128 x 128 block tile
+  static constexpr int WM = 2, WN = 2, SM = 2, SN = 2;  // 128 items × 128 queries
 };
 
-int gemm_tile_m(int dtype) {
-  return dtype == BF16 ? CfgBF16::WM * CfgBF16::SM * 32
-                       : CfgF32::WM * CfgF32::SM * 32;
+int gemm_tile_m(int dtype) {  // queries per block (Mpad multiple)
+  return dtype == BF16 ? CfgBF16::WN * CfgBF16::SN * 32 : CfgF32::WN * CfgF32::SN * 32;
 }
-int gemm_tile_n(int dtype) {
-  return dtype == BF16 ? CfgBF16::WN * CfgBF16::SN * 32
-                       : CfgF32::WN * CfgF32::SN * 32;
+int gemm_tile_n(int dtype) {  // items per block (Ncols multiple)
+  return dtype == BF16 ? CfgBF16::WM * CfgBF16::SM * 32 : CfgF32::WM * CfgF32::SM * 32;
 }
 int gemm_tile_k(int dtype) { return dtype == BF16 ? 64 : 32; }
 
+template <typename T, int KU>
+static void launch_scan_t(const GemmArgs& a, hipStream_t s) {
+  const int n_groups = a.Mpad / (kScanWaves * 32);
+  const int tiles = a.Ncols / 32;
+  // one workgroup per CU (LDS + VGPR budget): ~256 workgroups, chunks balanced to ±1 tile
+  int n_chunks = (256 + n_groups - 1) / n_groups;
+  n_chunks = n_chunks < tiles ? n_chunks : tiles;
+  hipLaunchKernelGGL((scan_kernel<T, KU>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks,
+                     tiles);
+}
+
+template <typename T>
+static bool launch_scan(const GemmArgs& a, hipStream_t s) {
+  const int ku = (int)(a.Kpad * sizeof(T) / 16);
+  switch (ku) {
+    case 8: launch_scan_t<T, 8>(a, s); return true;
+    case 16: launch_scan_t<T, 16>(a, s); return true;
+    case 24: launch_scan_t<T, 24>(a, s); return true;
+    case 32: launch_scan_t<T, 32>(a, s); return true;
+    case 48: launch_scan_t<T, 48>(a, s); return true;
+    case 64: launch_scan_t<T, 64>(a, s); return true;
+    case 96: launch_scan_t<T, 96>(a, s); return true;
+    default: return false;
+  }
+}
+
+bool scan_supported(int dtype, int Kpad) {
+  const int ku = Kpad * (dtype == BF16 ? 2 : 4) / 16;
+  return ku == 8 || ku == 16 || ku == 24 || ku == 32 || ku == 48 || ku == 64 || ku == 96;
+}
+
 hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   const int bm = gemm_tile_m(dtype), bn = gemm_tile_n(dtype), bk = gemm_tile_k(dtype);
-  if (a.Mpad % bm || a.Ncols % bn || a.Kpad % bk || a.Mpad <= 0 || a.Ncols <= 0) return hipErrorInvalidValue;
+  if (a.Mpad % bm || a.Ncols % bn || a.Kpad % bk || a.Mpad <= 0 || a.Ncols <= 0 || (a.slab_start & 31))
+    return hipErrorInvalidValue;
+  if (a.Mpad % (kScanWaves * 32) == 0 && scan_supported(dtype, a.Kpad) && !getenv("BB_FORCE_TILED_GEMM")) {
+    if (dtype == BF16 ? launch_scan<uint16_t>(a, s) : launch_scan<float>(a, s)) return hipGetLastError();
+  }
   const int blocks = (a.Mpad / bm) * (a.Ncols / bn);
   if (dtype == BF16) {
     constexpr int nt = CfgBF16::WM * CfgBF16::WN * 64;
-    hipLaunchKernelGGL((gemm_nt_kernel<uint16_t, CfgBF16::WM, CfgBF16::WN, CfgBF16::SM, CfgBF16::SN>), dim3(blocks), dim3(nt), 0, s, a);
+    hipLaunchKernelGGL((gemm_nt_kernel<uint16_t, CfgBF16::WM, CfgBF16::WN, CfgBF16::SM, CfgBF16::SN>),
+                       dim3(blocks), dim3(nt), 0, s, a);
   } else {
     constexpr int nt = CfgF32::WM * CfgF32::WN * 64;
-    hipLaunchKernelGGL((gemm_nt_kernel<float, CfgF32::WM, CfgF32::WN, CfgF32::SM, CfgF32::SN>), dim3(blocks), dim3(nt), 0, s, a);
+    hipLaunchKernelGGL((gemm_nt_kernel<float, CfgF32::WM, CfgF32::WN, CfgF32::SM, CfgF32::SN>), dim3(blocks),
+                       dim3(nt), 0, s, a);
   }
   return hipGetLastError();
 }

@@ -6,28 +6,29 @@
 // row.  Eligible = in the slab ∧ present bit (structural: the side's item space) ∧ mask
 // bit (valid_set_filter, :229/:454) ∧ ¬exclusion bit (items the user rated, :441-451).
 //
-// Fast path (bound + filter + sort):
-//   pass 1  stage the row's order-images in LDS (0 = ineligible), track each thread's max
-//           and the unmasked arg-max key (rank 0 of the reference's argsort, :217)
-//   bound   T0 = the K-th largest per-thread max (and the carried list's K-th key): at
-//           least K eligible elements are >= T0, so every member of the top K is too
-//   pass 2  append every element with order-image >= T0 (typically ~K..2K of them)
+// Inputs from the GEMM epilogue: per (query, 32-item tile) the maximum order-image over
+// eligible items (tmax) and over present items (pmax, similar-sets only).
+//   rank 0  the unmasked arg-max key (dropped by the similar-sets path, :217) = the first
+//           present item holding the largest pmax, found by reading one tile
+//   bound   T0 = the K-th largest per-thread max of tmax (and the carried list's K-th key):
+//           at least K eligible items are >= T0, so every top-K member is
+//   gather  read only the tiles with tmax >= T0 (~K of N/32), append eligible items >= T0
 //   sort    bitonic sort of the candidates by the full key (score desc, id asc) -> top K
-// Exact fallback (candidates overflow the LDS buffer, e.g. masses of equal scores):
-//   3-level radix select (12/12/8 bits) for the K-th score T, take everything above T and
-//   the ties at T in ascending global id (carried keys first: earlier slabs = smaller ids).
+// Exact fallback (candidates overflow the LDS buffer, e.g. masses of equal scores): a
+//   3-level radix select (12/12/8 bits) over the whole row for the K-th score T; take all
+//   above T and the ties at T in ascending global id (carried keys first: earlier slabs
+//   hold smaller ids).
 #include "common.h"
 
 namespace bb {
 
-constexpr int kCandCap = 2048;                  // fast-path candidate capacity
+constexpr int kCandCap = 2048;                  // candidate capacity
 constexpr int kOffHist = kMaxKInt * 8;          // radix path: cand[0..kMaxKInt) then hist
 constexpr int kRegionA = kOffHist + 4096 * 4;   // 20 KiB, reused by both paths
 static_assert(kCandCap * 8 <= kRegionA, "candidate buffer must fit region A");
 constexpr int kOffTmax = kRegionA;              // u32[256] per-thread maxima
 constexpr int kOffMisc = kOffTmax + kSelectThreads * 4;
-constexpr int kOffOrds = kOffMisc + 256;        // staged row
-constexpr size_t kSelectFixedLds = kOffOrds;
+constexpr int kSelectLds = kOffMisc + 256;
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -96,15 +97,16 @@ __device__ __forceinline__ void bitonic_desc_u64(uint64_t* v, int P) {
     }
 }
 
-// Exact radix fallback over the staged row (+ carried keys).  Leaves cnt (<= K) keys in
-// cand[0..cnt) and returns cnt.
-__device__ uint32_t radix_select(const uint32_t* ords, int n, uint32_t gid0, const uint64_t* carry, int K,
-                                 uint64_t* cand, uint32_t* hist, uint32_t* misc, uint32_t* scan_sh) {
+// Exact radix fallback over the whole row (+ carried keys); ord_at(j) = order-image of
+// column j or 0 when ineligible.  Leaves cnt (<= K) keys in cand[0..cnt), returns cnt.
+template <typename OrdAt>
+__device__ uint32_t radix_select(OrdAt ord_at, int n, uint32_t gid0, const uint64_t* carry, int K, uint64_t* cand,
+                                 uint32_t* hist, uint32_t* misc, uint32_t* scan_sh) {
   const int tid = threadIdx.x;
   for (int i = tid; i < 4096; i += kSelectThreads) hist[i] = 0;
   __syncthreads();
   for (int j = tid; j < n; j += kSelectThreads) {
-    const uint32_t o = ords[j];
+    const uint32_t o = ord_at(j);
     if (o) atomicAdd(&hist[o >> 20], 1u);
   }
   if (carry)
@@ -122,7 +124,7 @@ __device__ uint32_t radix_select(const uint32_t* ords, int n, uint32_t gid0, con
     for (int i = tid; i < 4096; i += kSelectThreads) hist[i] = 0;
     __syncthreads();
     for (int j = tid; j < n; j += kSelectThreads) {
-      const uint32_t o = ords[j];
+      const uint32_t o = ord_at(j);
       if (o && (o >> 20) == b1) atomicAdd(&hist[(o >> 8) & 0xFFFu], 1u);
     }
     if (carry)
@@ -138,7 +140,7 @@ __device__ uint32_t radix_select(const uint32_t* ords, int n, uint32_t gid0, con
     for (int i = tid; i < 256; i += kSelectThreads) hist[i] = 0;
     __syncthreads();
     for (int j = tid; j < n; j += kSelectThreads) {
-      const uint32_t o = ords[j];
+      const uint32_t o = ord_at(j);
       if (o && (o >> 8) == p24) atomicAdd(&hist[o & 0xFFu], 1u);
     }
     if (carry)
@@ -160,7 +162,7 @@ __device__ uint32_t radix_select(const uint32_t* ords, int n, uint32_t gid0, con
   __syncthreads();
   const uint32_t lo = ordered_ties ? T + 1u : T;  // take ords >= lo without ordering
   for (int j = tid; j < n; j += kSelectThreads) {
-    const uint32_t o = ords[j];
+    const uint32_t o = ord_at(j);
     if (o && o >= lo) cand[atomicAdd(&misc[4], 1u)] = make_key(o, gid0 + (uint32_t)j);
   }
   if (carry)
@@ -188,7 +190,7 @@ __device__ uint32_t radix_select(const uint32_t* ords, int n, uint32_t gid0, con
     uint32_t rem = misc[5];
     for (int base = 0; base < n && rem; base += kSelectThreads) {
       const int j = base + tid;
-      const uint32_t o = j < n ? ords[j] : 0u;
+      const uint32_t o = j < n ? ord_at(j) : 0u;
       const uint32_t tie = (o == T) ? 1u : 0u;
       uint32_t tot;
       const uint32_t rk = block_excl_scan(tie, scan_sh, tot);
@@ -203,81 +205,155 @@ __device__ uint32_t radix_select(const uint32_t* ords, int n, uint32_t gid0, con
 }
 
 __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  __shared__ __attribute__((aligned(16))) char dsm[kSelectLds];
   uint64_t* cand = (uint64_t*)dsm;
   uint32_t* hist = (uint32_t*)(dsm + kOffHist);
-  uint32_t* tmax = (uint32_t*)(dsm + kOffTmax);
+  uint32_t* tmx = (uint32_t*)(dsm + kOffTmax);
   uint32_t* misc = (uint32_t*)(dsm + kOffMisc);  // [0..15] scalars
   uint32_t* scan_sh = misc + 16;                  // 8 words
   uint64_t* red = (uint64_t*)(misc + 32);         // 4 u64
-  uint32_t* ords = (uint32_t*)(dsm + kOffOrds);
 
-  const int row = blockIdx.x, tid = threadIdx.x;
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int n = a.n_cols, K = a.K;
+  const int ntiles = (n + 31) >> 5;
   const float* Srow = a.S + (size_t)row * a.lds;
+  const uint32_t* trow = a.tmax + (size_t)row * a.ldt;
   const uint32_t* excl = a.excl ? a.excl + (size_t)row * a.excl_ld : nullptr;
   const uint64_t* carry = a.carry_in ? a.carry_in + (size_t)row * K : nullptr;
 
-  // ---- pass 1: stage order-images, per-thread max, unmasked arg-max ----
-  uint64_t lmax = 0;
-  uint32_t tm = 0;
-  for (int j = tid; j < n; j += kSelectThreads) {
-    const int64_t li = a.slab_start + j;
-    const int64_t w = li >> 5;
-    const uint32_t bit = 1u << (li & 31);
-    const uint32_t o = ord_of(Srow[j]);
-    const bool pr = !a.present || (a.present[w] & bit);
-    if (pr) {
-      const uint64_t key = make_key(o, a.gid0 + (uint32_t)j);
-      lmax = key > lmax ? key : lmax;
-    }
-    const bool e = pr && (!a.mask || (a.mask[w] & bit)) && !(excl && (excl[w] & bit));
-    const uint32_t oe = e ? o : 0u;
-    ords[j] = oe;
-    tm = oe > tm ? oe : tm;
-  }
-  tmax[tid] = tm;
-  if (a.max_inout) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const uint64_t y = __shfl_xor(lmax, o);
-      lmax = y > lmax ? y : lmax;
-    }
-    if ((tid & 63) == 0) red[tid >> 6] = lmax;
-  }
+  auto words = [&](int tile, uint32_t& pw, uint32_t& mw, uint32_t& ew) {
+    const int64_t w = (a.slab_start >> 5) + tile;
+    pw = a.present ? a.present[w] : ~0u;
+    mw = a.mask ? a.mask[w] : ~0u;
+    ew = excl ? excl[w] : 0u;
+  };
+
   if (tid == 0) {
     misc[6] = 0;  // T0 (atomicMax)
     misc[7] = 0;  // candidate count
+    *(uint64_t*)(misc + 10) = 0ull;  // running rank-0 key
   }
   __syncthreads();
-  if (a.max_inout && tid == 0) {
-    uint64_t m = a.first_slab ? 0ull : a.max_inout[row];
-    for (int i = 0; i < kSelectThreads / 64; ++i) m = red[i] > m ? red[i] : m;
-    a.max_inout[row] = m;
+
+  // ---- rank 0: first present item holding the largest present maximum ----
+  if (a.max_inout) {
+    const uint32_t* prow = a.pmax + (size_t)row * a.ldt;
+    uint64_t best = 0;  // (ord << 32) | ~tile : larger = higher ord, then lower tile
+    for (int t0 = tid; t0 < ntiles; t0 += 4 * kSelectThreads) {
+      uint32_t pv[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int t = t0 + b * kSelectThreads;
+        pv[b] = t < ntiles ? prow[t] : 0u;
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int t = t0 + b * kSelectThreads;
+        const uint64_t v = ((uint64_t)pv[b] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)t);
+        best = (pv[b] && v > best) ? v : best;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t y = __shfl_xor(best, o);
+      best = y > best ? y : best;
+    }
+    if (lane == 0) red[tid >> 6] = best;
+    __syncthreads();
+    if (tid < 64) {
+      uint64_t b = red[0];
+      for (int i = 1; i < kSelectThreads / 64; ++i) b = red[i] > b ? red[i] : b;
+      const uint32_t P = (uint32_t)(b >> 32);
+      uint64_t key = 0;
+      if (P) {
+        const int t = (int)(0xFFFFFFFFu - (uint32_t)b);
+        const int j = t * 32 + (lane & 31);
+        uint32_t pw, mw, ew;
+        words(t, pw, mw, ew);
+        const bool hit = lane < 32 && j < n && ((pw >> (lane & 31)) & 1u) && ord_of(Srow[j]) == P;
+        const uint64_t m = __ballot(hit);
+        if (m) key = make_key(P, a.gid0 + (uint32_t)(t * 32 + __builtin_ctzll(m)));
+      }
+      if (tid == 0) {
+        const uint64_t prev = a.first_slab ? 0ull : a.max_inout[row];
+        const uint64_t m = key > prev ? key : prev;
+        a.max_inout[row] = m;
+        *(uint64_t*)(misc + 10) = m;  // for the final-output drop below
+      }
+    }
   }
 
-  // ---- bound: T0 = K-th largest per-thread max (ties: count of values >= mine) ----
-  if (tm) {
+  // ---- bound: T0 = K-th largest per-thread max of the tile maxima ----
+  // (loads batched kB per thread so one memory latency covers kB tiles)
+  constexpr int kB = 4;
+  uint32_t tm = 0;
+  uint32_t v0[kB];  // the first batch stays in registers for the gather below
+#pragma unroll
+  for (int b = 0; b < kB; ++b) {
+    const int t = tid + b * kSelectThreads;
+    v0[b] = t < ntiles ? trow[t] : 0u;
+    tm = v0[b] > tm ? v0[b] : tm;
+  }
+  for (int t0 = tid + kB * kSelectThreads; t0 < ntiles; t0 += kB * kSelectThreads) {
+    uint32_t v[kB];
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+      const int t = t0 + b * kSelectThreads;
+      v[b] = t < ntiles ? trow[t] : 0u;
+    }
+#pragma unroll
+    for (int b = 0; b < kB; ++b) tm = v[b] > tm ? v[b] : tm;
+  }
+  tmx[tid] = tm;
+  __syncthreads();
+  if (tm) {  // rank of my maximum among the 256 (16-B LDS reads, all independent)
     uint32_t ge = 0;
-    for (int t = 0; t < kSelectThreads; ++t) ge += tmax[t] >= tm ? 1u : 0u;
+#pragma unroll 8
+    for (int t = 0; t < kSelectThreads; t += 4) {
+      const uint4 v = *(const uint4*)(tmx + t);
+      ge += (v.x >= tm) + (v.y >= tm) + (v.z >= tm) + (v.w >= tm);
+    }
     if (ge >= (uint32_t)K) atomicMax(&misc[6], tm);
   }
   __syncthreads();
   uint32_t T0 = misc[6];
-  if (carry && K > 0) {
-    const uint32_t ck = ordk_of(carry[K - 1]);  // K carried keys >= ck
+  if (carry) {
+    const uint32_t ck = ordk_of(carry[K - 1]);  // K carried keys are >= ck
     T0 = ck > T0 ? ck : T0;
   }
-  if (T0 == 0) T0 = 1;  // fewer than K threads hold eligible items: take every eligible one
+  if (T0 == 0) T0 = 1;  // fewer than K threads see eligible items: take every eligible one
 
-  // ---- pass 2: candidates >= T0 ----
-  for (int j = tid; j < n; j += kSelectThreads) {
-    const uint32_t o = ords[j];
-    if (o >= T0) {
-      const uint32_t p = atomicAdd(&misc[7], 1u);
-      if (p < kCandCap) cand[p] = make_key(o, a.gid0 + (uint32_t)j);
+  // ---- gather: only tiles whose eligible max reaches T0 ----
+  // Qualifying tiles (~K per row) are spread over the threads; a thread issues its tile's
+  // eight 16-B score loads at once.  The first batch of tile maxima is still in registers.
+  auto gather_tile = [&](int t) {
+    uint32_t pw, mw, ew;
+    words(t, pw, mw, ew);
+    const uint32_t ok = pw & mw & ~ew;
+    float4 v[8];
+#pragma unroll
+    for (int c4 = 0; c4 < 8; ++c4) v[c4] = *(const float4*)(Srow + t * 32 + 4 * c4);
+#pragma unroll
+    for (int c4 = 0; c4 < 8; ++c4) {
+      const float f[4] = {v[c4].x, v[c4].y, v[c4].z, v[c4].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int it = 4 * c4 + c, j = t * 32 + it;
+        const uint32_t o = ord_of(f[c]);
+        if (j < n && ((ok >> it) & 1u) && o >= T0) {
+          const uint32_t p = atomicAdd(&misc[7], 1u);
+          if (p < kCandCap) cand[p] = make_key(o, a.gid0 + (uint32_t)j);
+        }
+      }
     }
+  };
+#pragma unroll
+  for (int b = 0; b < kB; ++b) {
+    const int t = tid + b * kSelectThreads;
+    if (t < ntiles && v0[b] >= T0) gather_tile(t);
   }
+  for (int t = tid + kB * kSelectThreads; t < ntiles; t += kSelectThreads)
+    if (trow[t] >= T0) gather_tile(t);
   if (carry)
     for (int c = tid; c < K; c += kSelectThreads) {
       const uint64_t key = carry[c];
@@ -290,7 +366,13 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   uint32_t cnt = misc[7];
   if (cnt > (uint32_t)kCandCap) {
     __syncthreads();
-    cnt = radix_select(ords, n, a.gid0, carry, K, cand, hist, misc, scan_sh);
+    auto ord_at = [&](int j) -> uint32_t {
+      uint32_t pw, mw, ew;
+      words(j >> 5, pw, mw, ew);
+      const int it = j & 31;
+      return (((pw & mw & ~ew) >> it) & 1u) ? ord_of(Srow[j]) : 0u;
+    };
+    cnt = radix_select(ord_at, n, a.gid0, carry, K, cand, hist, misc, scan_sh);
   }
 
   // ---- sort candidates by full key, emit the top K ----
@@ -299,26 +381,37 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   for (int i = (int)cnt + tid; i < P; i += kSelectThreads) cand[i] = 0ull;
   __syncthreads();
   bitonic_desc_u64(cand, P);
+  if (a.out_scores) {
+    // final list of a single-list mode (semantic / similar / CF) on its last slab: drop
+    // rank 0 when it is the head of the list (a present-but-masked rank 0 is not in it),
+    // then emit k_final (score, id) pairs — what finalize does for one shard.
+    const uint64_t gmax = *(const uint64_t*)(misc + 10);  // set by tid 0 above (0 = no drop)
+    const int start = (gmax && cnt && cand[0] == gmax) ? 1 : 0;
+    const int c = min(a.k_final, (int)cnt - start);
+    float* sc = a.out_scores + (size_t)row * a.k_final;
+    int64_t* id = a.out_ids + (size_t)row * a.k_final;
+    for (int i = tid; i < a.k_final; i += kSelectThreads) {
+      if (i < c) {
+        const uint64_t key = cand[start + i];
+        sc[i] = float_of_ord(ordk_of(key));
+        id[i] = (int64_t)gid_of(key);
+      } else {
+        sc[i] = 0.f;
+        id[i] = -1;
+      }
+    }
+    if (a.out_counts && tid == 0) a.out_counts[row] = c;
+    return;
+  }
   uint64_t* out = a.keys_out + (size_t)row * K;
   for (int i = tid; i < K; i += kSelectThreads) out[i] = i < (int)cnt ? cand[i] : 0ull;
 }
 
-static int g_select_attr_dev = -1;
-
 hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s) {
-  if (a.K <= 0 || a.K > kMaxKInt || B <= 0 || a.n_cols <= 0 || a.n_cols > kSelectStageMax)
+  if (a.K <= 0 || a.K > kMaxKInt || B <= 0 || a.n_cols <= 0 || !a.tmax || (a.max_inout && !a.pmax) ||
+      (a.slab_start & 31))
     return hipErrorInvalidValue;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (g_select_attr_dev != dev) {
-    e = hipFuncSetAttribute((const void*)select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kSelectFixedLds + (size_t)kSelectStageMax * 4));
-    if (e != hipSuccess) return e;
-    g_select_attr_dev = dev;
-  }
-  const size_t bytes = kSelectFixedLds + (size_t)((a.n_cols + 3) & ~3) * 4;
-  hipLaunchKernelGGL(select_kernel, dim3(B), dim3(kSelectThreads), bytes, s, a);
+  hipLaunchKernelGGL(select_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
   return hipGetLastError();
 }
 

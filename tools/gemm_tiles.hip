@@ -30,13 +30,17 @@ struct Variant {
   void (*launch)(const GemmArgs&, int blocks, hipStream_t);
 };
 
-template <typename T, int WM, int WN, int SM, int SN>
+template <typename T, int WM, int WN, int SM, int SN, int RB>
 void launch_v(const GemmArgs& a, int blocks, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_nt_kernel<T, WM, WN, SM, SN>), dim3(blocks), dim3(WM * WN * 64), 0, s, a);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, WM, WN, SM, SN, RB>), dim3(blocks), dim3(WM * WN * 64), 0, s, a);
 }
 
-#define V(T, WM, WN, SM, SN) \
-  Variant { #T "_" #WM "x" #WN "w_" #SM "x" #SN "t", WM * SM * 32, WN * SN * 32, WM * WN * 64, launch_v<T, WM, WN, SM, SN> }
+// bm = queries per block (WN*SN*32), bn = items per block (WM*SM*32)
+#define V(T, WM, WN, SM, SN, RB)                                                                 \
+  Variant {                                                                                      \
+    #T "_" #WM "x" #WN "w_" #SM "x" #SN "t_kb" #RB, WN * SN * 32, WM * SM * 32, WM * WN * 64,    \
+        launch_v<T, WM, WN, SM, SN, RB>                                                          \
+  }
 
 static uint16_t f2bf(float f) {
   uint32_t u;
@@ -50,11 +54,11 @@ int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 30;
   const int rounds = 5;
   std::vector<int> Ms = {256, 1024, 4096};
-  std::vector<Variant> vf = {V(float, 2, 2, 1, 1), V(float, 2, 2, 1, 2), V(float, 2, 2, 2, 1),
-                             V(float, 2, 2, 2, 2), V(float, 1, 4, 2, 1), V(float, 4, 1, 1, 2),
-                             V(float, 2, 4, 1, 1)};
-  std::vector<Variant> vb = {V(uint16_t, 2, 2, 2, 2), V(uint16_t, 2, 2, 1, 1), V(uint16_t, 2, 2, 2, 1),
-                             V(uint16_t, 2, 2, 1, 2), V(uint16_t, 2, 4, 2, 2), V(uint16_t, 4, 2, 2, 2)};
+  std::vector<Variant> vf = {V(float, 2, 2, 1, 1, 128), V(float, 2, 2, 1, 1, 256), V(float, 2, 2, 2, 2, 128),
+                             V(float, 2, 2, 2, 2, 256), V(float, 2, 4, 1, 1, 128), V(float, 2, 4, 1, 1, 256),
+                             V(float, 4, 2, 1, 1, 256), V(float, 2, 2, 2, 1, 256), V(float, 2, 2, 1, 2, 256)};
+  std::vector<Variant> vb = {V(uint16_t, 2, 2, 2, 2, 128), V(uint16_t, 2, 2, 2, 2, 256), V(uint16_t, 2, 4, 2, 2, 128),
+                             V(uint16_t, 4, 2, 2, 2, 128), V(uint16_t, 2, 2, 1, 2, 256), V(uint16_t, 2, 2, 2, 1, 256)};
   const int Mmax = 4096;
   std::vector<float> hq((size_t)Mmax * D), hx((size_t)N * D);
   srand(1);

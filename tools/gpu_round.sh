@@ -1,11 +1,14 @@
 #!/bin/bash
-# parity tests -> tile micro-bench -> bench; stop at any abnormal exit
+# parity tests -> bench -> probes; stop at any abnormal exit
 set -u
 mkdir -p gpurun_out
 bash tools/gpu_check.sh; rc=$?
 if [ $rc -ne 0 ]; then exit $rc; fi
-if [ -x tools/gemm_tiles ]; then
-  timeout -k 10 300 ./tools/gemm_tiles 20 > gpurun_out/gemm_tiles.jsonl 2> gpurun_out/gemm_tiles.err; rc=$?
-  echo "gemm_tiles rc=$rc"; cat gpurun_out/gemm_tiles.jsonl; tail -3 gpurun_out/gemm_tiles.err
-fi
-exit $rc
+for t in scan_probe; do
+  if [ -x tools/$t ]; then
+    timeout -k 10 200 ./tools/$t > gpurun_out/$t.jsonl 2> gpurun_out/$t.err; rc=$?
+    echo "$t rc=$rc"; cat gpurun_out/$t.jsonl; tail -3 gpurun_out/$t.err
+    [ $rc -ne 0 ] && exit $rc
+  fi
+done
+exit 0
