@@ -1,0 +1,109 @@
+"""Host-side logic of the drop-in, CPU only: bitset packing, the constraint -> Predicate
+compiler (checked against the reference's own apply_constraints masks in G4 through a
+numpy evaluation of the Predicate with the mask kernel's semantics), LIKE matching and the
+reference's constraint helper functions."""
+import json
+
+import numpy as np
+import pytest
+
+from _spaces import catalog_json
+from brickrec.constraints import (ConstraintType, HardConstraint, create_age_appropriate_constraints,
+                                  create_budget_constraints, create_constraint_set_values,
+                                  create_size_constraints, predicate_from_constraints, theme_ids_like)
+from brickrec.engine import INT32_MAX, INT32_MIN, Predicate, bits_from_bool, bool_from_bits
+
+
+def eval_predicate(p: Predicate, parts, year, theme, n_ids=None):
+    """numpy statement of mask_kernel (csrc/misc.hip): inclusive bounds, num_parts > 0,
+    theme tests with SQL NULL (theme < 0) -> false, then excluded ids cleared."""
+    parts, year, theme = (np.asarray(a, np.int64) for a in (parts, year, theme))
+    m = (parts > 0) & (parts >= p.parts_min) & (parts <= p.parts_max)
+    m &= (year >= p.year_min) & (year <= p.year_max)
+    if p.theme_mode:
+        inset = np.isin(theme, list(p.theme_ids))
+        m &= (theme >= 0) & (inset if p.theme_mode == 1 else ~inset)
+    if len(p.excluded_items):
+        m[np.asarray(p.excluded_items, np.int64)] = False
+    return m
+
+
+@pytest.mark.parametrize("n", [0, 1, 31, 32, 33, 1000])
+def test_bits_round_trip(n):
+    rng = np.random.default_rng(n)
+    m = rng.random(n) < 0.3
+    w = bits_from_bool(m)
+    assert w.dtype == np.uint32 and w.shape == ((n + 31) // 32,)
+    assert np.array_equal(bool_from_bits(w, n), m)
+    for i in np.flatnonzero(m):
+        assert (w[i // 32] >> (i % 32)) & 1
+
+
+def test_bits_batched():
+    m = np.zeros((3, 70), bool)
+    m[1, 69] = m[2, 0] = True
+    w = bits_from_bool(m)
+    assert w.shape == (3, 3)
+    assert w[1, 2] == 1 << 5 and w[2, 0] == 1
+
+
+def test_predicate_compiler_matches_reference_masks(golden):
+    g1, g4 = golden("g1_content.npz"), golden("g4_hybrid.npz")
+    cat = catalog_json()
+    themes = {int(k): v for k, v in cat["themes"].items()}
+    owned = {3: set(int(i) for i in g4["owned_rows"])}
+    wished = {3: set(int(i) for i in g4["wished_rows"])}
+    for ci, cj in enumerate(g4["case_json"]):
+        kw = json.loads(str(cj))
+        pred = predicate_from_constraints(create_constraint_set_values(**kw), themes, owned, wished,
+                                          int(g4["current_year"]))
+        if pred is None:
+            m = np.zeros(len(g1["num_parts"]), bool)
+        else:
+            m = eval_predicate(pred, g1["num_parts"], g1["year"], g1["theme_id"])
+        assert np.array_equal(m, g4["masks"][ci]), f"case {ci} {kw}"
+
+
+def test_predicate_int32_ranges():
+    p = predicate_from_constraints([], {}, {}, {}, 2025)
+    assert (p.parts_min, p.parts_max, p.year_min, p.year_max) == (INT32_MIN, INT32_MAX, INT32_MIN, INT32_MAX)
+    p = predicate_from_constraints(create_constraint_set_values(price_max=45.0, pieces_max=300), {}, {}, {}, 2025)
+    assert p.parts_max == 300
+    p = predicate_from_constraints(create_constraint_set_values(price_max=45.0, pieces_max=900), {}, {}, {}, 2025)
+    assert p.parts_max == int(45.0 / 0.10)
+    p = predicate_from_constraints(create_constraint_set_values(must_be_available=True), {}, {}, {}, 2025)
+    assert p.year_min == 2020
+
+
+def test_required_and_excluded_themes_combine():
+    names = {1: "Star Wars", 2: "Star Wars Ultimate", 3: "City", 4: "Technic"}
+    c = create_constraint_set_values(required_themes=["star wars"], excluded_themes=["ultimate"])
+    p = predicate_from_constraints(c, names, {}, {}, 2025)
+    assert p.theme_mode == 1 and list(p.theme_ids) == [1]
+    c = create_constraint_set_values(excluded_themes=["city", "zzz"])
+    p = predicate_from_constraints(c, names, {}, {}, 2025)
+    assert p.theme_mode == 2 and list(p.theme_ids) == [3]
+    assert predicate_from_constraints(create_constraint_set_values(required_themes=["zzz"]),
+                                      names, {}, {}, 2025) is None
+
+
+def test_like_semantics():
+    names = {1: "Star Wars", 2: "Harry_Potter", 3: "100% Fun", 4: "Space"}
+    assert theme_ids_like(names, ["STAR"]) == [1]
+    assert theme_ids_like(names, ["y_p"]) == [2]          # '_' matches one character
+    assert theme_ids_like(names, ["0%f"]) == [3]          # '%' matches any run
+    assert theme_ids_like(names, ["a"]) == [1, 2, 4]
+
+
+def test_constraint_helpers():
+    b = create_budget_constraints(100.0, 20.0)
+    assert [c.constraint_type for c in b] == [ConstraintType.PRICE_MAX, ConstraintType.PRICE_MIN]
+    a = create_age_appropriate_constraints(10)
+    assert a[0].constraint_type == ConstraintType.AGE_MIN and a[0].value == 8
+    assert create_age_appropriate_constraints(5, strict=False)[0].value == 4
+    s = create_size_constraints("Medium")
+    assert [(c.constraint_type, c.value) for c in s] == [(ConstraintType.PIECES_MIN, 201),
+                                                         (ConstraintType.PIECES_MAX, 800)]
+    assert create_size_constraints("huge") == []
+    h = HardConstraint(ConstraintType.PIECES_MAX, 10)
+    assert h.description == "pieces_max: 10"
