@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.join(ROOT, "brickbrain-rec-engine_amd"))
 N_ITEMS, DIM, BATCH, TOPK = 25216, 384, 256, 50
 PEAK = {"f32": ("mfma", 157.3, "TFLOP/s"), "bf16": ("mfma", 2500.0, "TFLOP/s")}
 HBM_PEAK_GBS = 8000.0
+KERNEL = {"f32": "scan_kernel<float,96>", "bf16": "scan_kernel<uint16_t,48>"}
 
 
 def unit_rows_torch(n, d, seed, device):
@@ -138,7 +139,7 @@ def main():
     gemm_us = 1e3 * g["ms"] / max(g["launches"], 1)
     flops = 2.0 * B * N_ITEMS * DIM
     es = 4 if args.dtype == "f32" else 2
-    alg_bytes = N_ITEMS * DIM * es + B * DIM * es + B * N_ITEMS * 4  # items + queries + score slab
+    alg_bytes = N_ITEMS * DIM * es + B * DIM * 4 + B * TOPK * 8    # items + queries + top-K out
     bound, peak, unit = PEAK[args.dtype]
     achieved = flops / (gemm_us * 1e-6) / 1e12
     hbm = load_pmc(args.dtype)
@@ -176,7 +177,8 @@ def main():
                    "parallelism": f"replicas x{world}" if world > 1 else "single"},
         "roofline": {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
                      "frac": round(achieved / peak, 4), "traffic": hbm,
-                     "kernel": "gemm_nt_kernel", "kernel_us": round(gemm_us, 3),
+                     "kernel": KERNEL[args.dtype] if not os.environ.get("BB_FORCE_TILED_GEMM") else "gemm_nt_kernel",
+                     "kernel_us": round(gemm_us, 3),
                      "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": alg_bytes,
                      "hbm_frac_at_alg_bytes": round(alg_bytes / (gemm_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
         "kernels_us_per_step": {k: round(1e3 * v["ms"] / max(args.steps, 1), 3) for k, v in prof.items()
