@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.join(ROOT, "brickbrain-rec-engine_amd"))
 N_ITEMS, DIM, BATCH, TOPK = 25216, 384, 256, 50
 PEAK = {"f32": ("mfma", 157.3, "TFLOP/s"), "bf16": ("mfma", 2500.0, "TFLOP/s")}
 HBM_PEAK_GBS = 8000.0
-KERNEL = {"f32": "scan_kernel<float,96>", "bf16": "scan_kernel<uint16_t,48>"}
+KERNEL = {"f32": "scan2_kernel<float,96>", "bf16": "scan2_kernel<uint16_t,48>"}
 
 
 def unit_rows_torch(n, d, seed, device):

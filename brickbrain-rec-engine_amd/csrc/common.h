@@ -51,6 +51,14 @@ struct GemmArgs {
   uint32_t* tmax;           // [Mpad][ldt] eligible max order-image per 32-item tile
   uint32_t* pmax;           // [Mpad][ldt] present max order-image (rank-0 search) or null
   int64_t ldt;
+  // fused query prologue (scan2): when set, Q is not read
+  const int64_t* q_ids;     // gather item rows of these global ids (minus q_id_offset)
+  int64_t q_id_offset, q_n_items;
+  const void* q_items_base; // full item matrix (row stride ldx)
+  const void* q_src;        // raw f32 query rows [M_valid][q_src_ld]
+  int64_t q_src_ld;
+  int32_t q_d;              // real query width (chunks past it read as 0)
+  int32_t q_normalize;      // L2-normalise q_src rows
 };
 
 struct SelectArgs {

@@ -24,7 +24,7 @@
 #include <cstdlib>
 
 #include "gemm_kernel.h"
-#include "scan_kernel.h"
+#include "scan2_kernel.h"
 
 namespace bb {
 
@@ -51,8 +51,13 @@ static void launch_scan_t(const GemmArgs& a, hipStream_t s) {
   // one workgroup per CU (LDS + VGPR budget): ~256 workgroups, chunks balanced to ±1 tile
   int n_chunks = (256 + n_groups - 1) / n_groups;
   n_chunks = n_chunks < tiles ? n_chunks : tiles;
-  hipLaunchKernelGGL((scan_kernel<T, KU>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks,
-                     tiles);
+  static const bool v1 = getenv("BB_SCAN_V1") != nullptr;
+  if (v1 && !a.q_ids && !a.q_src)
+    hipLaunchKernelGGL((scan_kernel<T, KU>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks,
+                       tiles);
+  else
+    hipLaunchKernelGGL((scan2_kernel<T, KU>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks,
+                       tiles);
 }
 
 template <typename T>

@@ -78,40 +78,99 @@ hipError_t launch_convert_rows(const void* src, int src_dtype, int64_t n, int d,
 // normalised) item rows of the liked sets (similar-sets: the query IS feat_matrix[target],
 // recommendation_system.py:213), or copy user factor rows (CF, :435).  Rows >= B are zero.
 // ---------------------------------------------------------------------------------------
+// Load C elements per lane (i = base + lane + 64c, zero past `d`) with the dtype switch
+// outside the loads, so all C loads are in flight together.
+template <int C>
+__device__ __forceinline__ void load_chunk(const void* p, int dt, size_t sb, int base, int d, int lane,
+                                           double (&x)[C]) {
+  if (dt == F32) {
+    const float* q = (const float*)p + sb;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int i = base + lane + 64 * c;
+      x[c] = i < d ? (double)q[i] : 0.0;
+    }
+  } else if (dt == F64) {
+    const double* q = (const double*)p + sb;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int i = base + lane + 64 * c;
+      x[c] = i < d ? q[i] : 0.0;
+    }
+  } else {
+    const uint16_t* q = (const uint16_t*)p + sb;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int i = base + lane + 64 * c;
+      x[c] = i < d ? (double)__builtin_bit_cast(float, (uint32_t)q[i] << 16) : 0.0;
+    }
+  }
+}
+
+constexpr int kPrepC = 8;  // rows up to 512 wide stay in registers (one load round)
+
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= a.Bpad) return;
   const size_t ob = (size_t)row * a.Dpad;
-  if (row >= a.B) {
+  const void* src = a.src;
+  int sdt = a.src_dtype, d = a.d, norm_on = a.normalize;
+  size_t sb = (size_t)row * a.src_ld;
+  bool zero = row >= a.B;
+  if (!zero && a.item_ids) {  // stored rows are already normalised and padded
+    const int64_t lid = a.item_ids[row] - a.id_offset;
+    zero = !(lid >= 0 && lid < a.n_items);
+    src = a.items;
+    sdt = a.out_dtype;
+    d = a.Dpad;
+    norm_on = 0;
+    sb = zero ? 0 : (size_t)lid * a.Dpad;
+  }
+  if (zero) {
     for (int i = lane; i < a.Dpad; i += 64) store_elem(a.out, a.out_dtype, ob + i, 0.f);
     return;
   }
-  if (a.item_ids) {
-    const int64_t lid = a.item_ids[row] - a.id_offset;
-    const bool ok = lid >= 0 && lid < a.n_items;
-    for (int i = lane; i < a.Dpad; i += 64) {
-      const float v = ok ? load_elem(a.items, a.out_dtype, (size_t)lid * a.Dpad + i) : 0.f;
-      store_elem(a.out, a.out_dtype, ob + i, v);
+  if (a.Dpad <= 64 * kPrepC) {
+    double x[kPrepC];
+    load_chunk<kPrepC>(src, sdt, sb, 0, d, lane, x);
+    double norm = 1.0;
+    if (norm_on) {
+      double ss = 0.0;
+#pragma unroll
+      for (int c = 0; c < kPrepC; ++c) ss += x[c] * x[c];
+      ss = wave_sum(ss);
+      norm = sqrt(ss);
+      if (norm == 0.0) norm = 1.0;
+    }
+#pragma unroll
+    for (int c = 0; c < kPrepC; ++c) {
+      const int i = lane + 64 * c;
+      if (i < a.Dpad) store_elem(a.out, a.out_dtype, ob + i, (float)(x[c] / norm));
     }
     return;
   }
-  const size_t sb = (size_t)row * a.src_ld;
   double norm = 1.0;
-  if (a.normalize) {
+  if (norm_on) {
     double ss = 0.0;
-    for (int i = lane; i < a.d; i += 64) {
-      const double x = load_elem_d(a.src, a.src_dtype, sb + i);
-      ss += x * x;
+    for (int base = 0; base < d; base += 64 * kPrepC) {
+      double x[kPrepC];
+      load_chunk<kPrepC>(src, sdt, sb, base, d, lane, x);
+#pragma unroll
+      for (int c = 0; c < kPrepC; ++c) ss += x[c] * x[c];
     }
     ss = wave_sum(ss);
     norm = sqrt(ss);
     if (norm == 0.0) norm = 1.0;
   }
-  for (int i = lane; i < a.Dpad; i += 64) {
-    float v = 0.f;
-    if (i < a.d) v = (float)(load_elem_d(a.src, a.src_dtype, sb + i) / norm);
-    store_elem(a.out, a.out_dtype, ob + i, v);
+  for (int base = 0; base < a.Dpad; base += 64 * kPrepC) {
+    double x[kPrepC];
+    load_chunk<kPrepC>(src, sdt, sb, base, d, lane, x);
+#pragma unroll
+    for (int c = 0; c < kPrepC; ++c) {
+      const int i = base + lane + 64 * c;
+      if (i < a.Dpad) store_elem(a.out, a.out_dtype, ob + i, (float)(x[c] / norm));
+    }
   }
 }
 

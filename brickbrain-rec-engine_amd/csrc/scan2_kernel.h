@@ -1,0 +1,319 @@
+// scan2_kernel.h — query-resident MFMA scan with the epilogue woven into the MFMA stream.
+//
+// Same contract and data flow as scan_kernel.h (queries resident in VGPRs, 32-item tiles
+// staged by LDS-DMA into an XOR-swizzled double buffer, S + per-tile maxima epilogue),
+// restructured for the single wave per SIMD that this register budget allows:
+//   * tiles alternate between two accumulator sets (even / odd), so tile t-1's epilogue
+//     (accumulator reads, order images, S stores, tile maxima) and tile t+1's staging are
+//     issued as small slices BETWEEN tile t's MFMAs — the VALU / VMEM work runs in the
+//     MFMA issue shadows instead of serially between tiles;
+//   * LDS fragment addresses are 8 per-lane bases + immediate offsets (no per-step VALU);
+//   * staging is branch-free (the tile after the last one re-stages the last tile);
+//   * optional fused query prologue: raw f32 query rows are L2-normalised in-kernel
+//     (sklearn normalize semantics, f64 sum of squares), or liked-set item rows are
+//     gathered by id — replacing the separate prep kernel on the hot path.
+#pragma once
+#include <utility>
+
+#include "scan_kernel.h"
+
+namespace bb {
+
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+template <int... I, typename F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+// Query operand: 16-B chunk (2u + h) of this lane's query row into qf[u].
+template <typename T, int KU>
+__device__ __forceinline__ void scan2_load_queries(const GemmArgs& a, int q, int h, uint4 (&qf)[KU / 2]) {
+  constexpr int U = KU / 2;
+  if (q >= a.M_valid) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) qf[u] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  if (a.q_ids) {  // similar / hybrid: the stored (normalised, padded) item row of the liked set
+    const int64_t lid = a.q_ids[q] - a.q_id_offset;
+    const bool ok = lid >= 0 && lid < a.q_n_items;
+    const char* row = (const char*)a.q_items_base + (size_t)(ok ? lid : 0) * a.ldx * sizeof(T);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint4 v = *(const uint4*)(row + (2 * u + h) * 16);
+      qf[u] = ok ? v : make_uint4(0, 0, 0, 0);
+    }
+    return;
+  }
+  if (a.q_src) {  // raw f32 rows (T == float): normalise here
+    const float* row = (const float*)a.q_src + (size_t)q * a.q_src_ld;
+    const int d = a.q_d;
+    float4 x[U];  // (host guarantees d % 4 == 0, 16-B aligned rows): clamp, load, select
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k0 = (2 * u + h) * 4;
+      const float4 t = *(const float4*)(row + (k0 < d ? k0 : d - 4));
+      x[u] = k0 < d ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (a.q_normalize) {
+      double ss = 0.0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ss += (double)x[u].x * x[u].x;
+        ss += (double)x[u].y * x[u].y;
+        ss += (double)x[u].z * x[u].z;
+        ss += (double)x[u].w * x[u].w;
+      }
+      ss += __shfl_xor(ss, 32);
+      double nrm = sqrt(ss);
+      if (nrm == 0.0) nrm = 1.0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        x[u].x = (float)((double)x[u].x / nrm);
+        x[u].y = (float)((double)x[u].y / nrm);
+        x[u].z = (float)((double)x[u].z / nrm);
+        x[u].w = (float)((double)x[u].w / nrm);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      qf[u] = make_uint4(__float_as_uint(x[u].x), __float_as_uint(x[u].y), __float_as_uint(x[u].z),
+                         __float_as_uint(x[u].w));
+    return;
+  }
+  const char* qrow = (const char*)a.Q + (size_t)q * a.ldq * sizeof(T);
+#pragma unroll
+  for (int u = 0; u < U; ++u) qf[u] = *(const uint4*)(qrow + (2 * u + h) * 16);
+}
+
+// ABL (tools/scan_probe only): 1 = no epilogue, 2 = no staging after the first tile,
+// 4 = no per-tile wait + barrier.
+template <typename T, int KU, int ABL = 0>
+__global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, int n_chunks, int tiles_total) {
+  constexpr int U = KU / 2;               // u-steps per tile (16-B chunk pairs)
+  constexpr int ROWB = KU * 16;
+  constexpr int TILE_B = 32 * ROWB;
+  constexpr int G = (KU % 16 == 0) ? 8 : 4;  // u-steps sharing one swizzle period
+  constexpr int PIECES = KU / 8;          // 1 KiB LDS-DMA pieces per wave per tile
+  static_assert(ROWB <= kScanRowMax, "row too wide for the scan kernel");
+  static_assert(KU % 8 == 0, "KU must split into whole 1 KiB pieces per wave");
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_B];
+
+  const int n_groups = a.Mpad / (kScanWaves * 32);
+  const int total = n_groups * n_chunks;
+  const int L = blockIdx.x;
+  const int xcd = L & 7, local = L >> 3, q8 = total >> 3, r8 = total & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+  const int chunk = t / n_groups, group = t - chunk * n_groups;
+  const int tile_lo = (int)((int64_t)chunk * tiles_total / n_chunks);
+  const int tile_hi = (int)((int64_t)(chunk + 1) * tiles_total / n_chunks);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int q = group * kScanWaves * 32 + wave * 32 + r;
+  if (tile_lo >= tile_hi) return;  // uniform per workgroup
+
+  uint4 qf[U];
+  scan2_load_queries<T, KU>(a, q, h, qf);
+  float qa[sizeof(T) == 4 ? 4 * U : 1];  // f32: the operand as 4U scalars, pinned to AGPRs
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      qa[4 * u + 0] = __uint_as_float(qf[u].x);
+      qa[4 * u + 1] = __uint_as_float(qf[u].y);
+      qa[4 * u + 2] = __uint_as_float(qf[u].z);
+      qa[4 * u + 3] = __uint_as_float(qf[u].w);
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * U; ++i) asm volatile("" : "+a"(qa[i]));
+  }
+  u32x4v qv[sizeof(T) == 2 ? U : 1];  // bf16: the operand as 4-dword vectors, pinned to AGPRs
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      qv[u] = __builtin_bit_cast(u32x4v, qf[u]);
+      asm volatile("" : "+a"(qv[u]));
+    }
+  }
+
+  // LDS fragment bases: chunk (2u + h) ^ swz(r) of row r = rd[u % G] + (u / G)·G·32 bytes
+  const int swz = scan_swz<KU>(r);
+  int rd[G];
+#pragma unroll
+  for (int m = 0; m < G; ++m) rd[m] = r * ROWB + (((2 * m + h) ^ swz) << 4);
+
+  // LDS-DMA source offsets of this lane's 16 B in each of its pieces (tile-relative)
+  const char* Xg = (const char*)a.X;
+  const size_t ldxb = (size_t)a.ldx * sizeof(T);
+  uint32_t soff[PIECES];
+#pragma unroll
+  for (int p = 0; p < PIECES; ++p) {
+    const int mine = (wave * PIECES + p) * 1024 + lane * 16;
+    const int row = mine / ROWB;
+    const int ch = ((mine % ROWB) >> 4) ^ scan_swz<KU>(row);
+    soff[p] = (uint32_t)(row * ldxb + ch * 16);
+  }
+  // Issued as inline asm: the compiler's waitcnt pass would otherwise (conservatively)
+  // wait for the LDS-DMA to land before every later ds_read — i.e. expose the whole HBM
+  // latency of the next tile inside this one.  Completion is enforced explicitly by the
+  // vmcnt(0) + barrier at the end of each tile, before anyone reads the buffer.
+  const uint32_t lds_base = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+  auto stage_piece = [&](int tile, int buf, int p) __attribute__((always_inline)) {
+    const char* src = Xg + (size_t)tile * 32 * ldxb + soff[p];
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + buf * TILE_B + (wave * PIECES + p) * 1024);
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory", "m0");
+  };
+
+  const size_t w0 = (size_t)(a.slab_start >> 5);
+  const uint32_t* erow = a.excl + (size_t)(q < a.M_valid ? q : a.M_valid - 1) * a.excl_ld;
+  float* Srow = a.S + (size_t)q * a.lds;
+
+  // first tile
+#pragma unroll
+  for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  asm volatile("s_nop 4");
+
+  f32x16s accE0, accE1, accO0, accO1;
+  uint32_t pw = 0, mw = 0, ew = 0;     // eligibility words of the tile whose epilogue is pending
+  uint32_t nw_p = 0, nw_m = 0, nw_e = 0;
+
+  // One tile: MFMA chain over LDS buffer BUF into (c0, c1); interleaved: the epilogue of the
+  // previous tile held in (p0, p1) (EPI), this tile's eligibility words, the next tile's
+  // staging into BUF^1.
+  constexpr int kEpiSlices = 15 + PIECES;
+  auto tile_body = [&](auto BUF, auto EPI, int tile, f32x16s& c0, f32x16s& c1, const f32x16s& p0,
+                       const f32x16s& p1) __attribute__((always_inline)) {
+    constexpr int buf = decltype(BUF)::value;
+    constexpr bool epi = decltype(EPI)::value && !(ABL & 1);
+    const int ptile = tile - 1;
+    const int stile = tile + 1 < tile_hi ? tile + 1 : tile;  // branch-free staging target
+    float v[16];
+    uint32_t te = 0, tp = 0;
+    const uint32_t ok = pw & mw & ~ew;
+    const int ptile0 = ptile * 32;
+    // item fragments: ds_read issued two u-steps ahead of their MFMAs
+    auto frag = [&](int u) __attribute__((always_inline)) {
+      return *(const uint4*)(smem + buf * TILE_B + rd[u % G] + (u / G) * G * 32);
+    };
+    uint4 fq[3];
+    fq[0] = frag(0);
+    if constexpr (U > 1) fq[1] = frag(1);
+    static_for<U>([&](auto UU) {
+      constexpr int u = decltype(UU)::value;
+      if constexpr (u + 2 < U) fq[(u + 2) % 3] = frag(u + 2);
+      const uint4 fa = fq[u % 3];
+      // MFMAs as inline asm so the resident query operand stays in AGPRs (srcB may be an
+      // AGPR on gfx950); the VGPR file is left to the fragments and the woven epilogue.
+      if constexpr (sizeof(T) == 4) {
+        const float pa[4] = {__uint_as_float(fa.x), __uint_as_float(fa.y), __uint_as_float(fa.z),
+                             __uint_as_float(fa.w)};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          f32x16s& acc = (u & 1) ? c1 : c0;
+          if (u < 2 && c == 0)
+            asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, 0" : "=a"(acc) : "v"(pa[c]), "a"(qa[4 * u + c]));
+          else
+            asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(pa[c]), "a"(qa[4 * u + c]));
+        }
+      } else {
+        f32x16s& acc = (u & 1) ? c1 : c0;
+        const u32x4v fv = __builtin_bit_cast(u32x4v, fa);
+        if constexpr (u < 2)
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(fv), "a"(qv[u]));
+        else
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(fv), "a"(qv[u]));
+      }
+      // ---- slices scheduled on this u-step: slice s runs at u = min(U-1, s+2) ----
+      static_for<kEpiSlices>([&](auto SS) {
+        constexpr int s = decltype(SS)::value;
+        constexpr int su = (s + 2 < U) ? s + 2 : U - 1;
+        if constexpr (su == u) {
+          if constexpr (s < 8) {
+            if constexpr (epi) {
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                const int g = 2 * s + e;
+                v[g] = p0[g] + p1[g];
+                const int it = (g & 3) + 8 * (g >> 2) + 4 * h;
+                const uint32_t o = ord_of(v[g]);
+                const bool in = ptile0 + it < a.n_valid;
+                const uint32_t op = (in && ((pw >> it) & 1u)) ? o : 0u;
+                const uint32_t oe = (in && ((ok >> it) & 1u)) ? o : 0u;
+                tp = op > tp ? op : tp;
+                te = oe > te ? oe : te;
+              }
+            }
+          } else if constexpr (s == 8) {
+            if constexpr (epi) {
+              const uint32_t te2 = __shfl_xor(te, 32), tp2 = __shfl_xor(tp, 32);
+              te = te2 > te ? te2 : te;
+              tp = tp2 > tp ? tp2 : tp;
+            }
+          } else if constexpr (s < 13) {
+            if constexpr (epi) {
+              constexpr int j = s - 9;
+              *(float4*)(Srow + ptile0 + 8 * j + 4 * h) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+            }
+          } else if constexpr (s == 13) {
+            if constexpr (epi) {
+              a.tmax[(size_t)q * a.ldt + ptile] = te;
+              a.pmax[(size_t)q * a.ldt + ptile] = tp;
+            }
+          } else if constexpr (s == 14) {
+            nw_p = a.present[w0 + tile];
+            nw_m = a.mask[w0 + tile];
+            nw_e = erow[w0 + tile];
+          } else {
+            if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s - 15);
+          }
+        }
+      });
+    });
+    pw = nw_p;
+    mw = nw_m;
+    ew = nw_e;
+    if constexpr (!(ABL & 4)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  };
+
+  // final epilogue of the last tile (not overlapped)
+  auto last_epilogue = [&](int tile, const f32x16s& p0, const f32x16s& p1) __attribute__((always_inline)) {
+    if constexpr (ABL & 1) return;
+    float v[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) v[g] = p0[g] + p1[g];
+    scan_epilogue(a, Srow, q, h, tile, v, pw, mw, ew);
+  };
+
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using EY = std::integral_constant<bool, true>;
+  using EN = std::integral_constant<bool, false>;
+  tile_body(B0{}, EN{}, tile_lo, accE0, accE1, accO0, accO1);
+  int tile = tile_lo + 1;
+  for (;;) {
+    if (tile >= tile_hi) {
+      last_epilogue(tile - 1, accE0, accE1);
+      break;
+    }
+    tile_body(B1{}, EY{}, tile, accO0, accO1, accE0, accE1);
+    ++tile;
+    if (tile >= tile_hi) {
+      last_epilogue(tile - 1, accO0, accO1);
+      break;
+    }
+    tile_body(B0{}, EY{}, tile, accE0, accE1, accO0, accO1);
+    ++tile;
+  }
+}
+
+}  // namespace bb

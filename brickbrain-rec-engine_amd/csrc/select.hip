@@ -20,6 +20,8 @@
 //   hold smaller ids).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace bb {
 
 constexpr int kCandCap = 2048;                  // candidate capacity
@@ -27,7 +29,9 @@ constexpr int kOffHist = kMaxKInt * 8;          // radix path: cand[0..kMaxKInt)
 constexpr int kRegionA = kOffHist + 4096 * 4;   // 20 KiB, reused by both paths
 static_assert(kCandCap * 8 <= kRegionA, "candidate buffer must fit region A");
 constexpr int kOffTmax = kRegionA;              // u32[256] per-thread maxima
-constexpr int kOffMisc = kOffTmax + kSelectThreads * 4;
+constexpr int kTileCap = 1024;                  // qualifying-tile list capacity
+constexpr int kOffTlist = kOffTmax + kSelectThreads * 4;
+constexpr int kOffMisc = kOffTlist + kTileCap * 4;
 constexpr int kSelectLds = kOffMisc + 256;
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
@@ -204,108 +208,180 @@ __device__ uint32_t radix_select(OrdAt ord_at, int n, uint32_t gid0, const uint6
   return cnt;
 }
 
+// Register-resident bitonic sort of up to 64·E keys by one wave (element e = s·64 + lane
+// lives in v[s]); descending.  No LDS, no barriers.
+template <int E>
+__device__ __forceinline__ void wave_bitonic_desc(uint64_t (&v)[E], int lane) {
+#pragma unroll
+  for (int k = 2; k <= 64 * E; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+        const int js = j >> 6;
+#pragma unroll
+        for (int s = 0; s < E; ++s) {
+          if ((s & js) == 0) {
+            const bool desc = ((s * 64) & k) == 0;  // lane bits are below k here
+            const uint64_t x = v[s], y = v[s | js];
+            const bool sw = desc ? (x < y) : (x > y);
+            v[s] = sw ? y : x;
+            v[s | js] = sw ? x : y;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < E; ++s) {
+          const int e = s * 64 + lane;
+          const uint64_t y = __shfl_xor(v[s], j);
+          const bool lower = (lane & j) == 0;
+          const bool desc = (e & k) == 0;
+          const bool keep_max = lower == desc;
+          v[s] = keep_max ? (v[s] > y ? v[s] : y) : (v[s] < y ? v[s] : y);
+        }
+      }
+    }
+  }
+}
+
+// Sort cnt (<= 64·E) candidates with one wave and emit the final list / the key list.
+template <int E>
+__device__ void wave_sort_emit(const uint64_t* cand, int cnt, const SelectArgs& a, int row, uint64_t gmax) {
+  const int lane = threadIdx.x & 63;
+  uint64_t v[E];
+#pragma unroll
+  for (int s = 0; s < E; ++s) {
+    const int e = s * 64 + lane;
+    v[s] = e < cnt ? cand[e] : 0ull;
+  }
+  wave_bitonic_desc<E>(v, lane);
+  if (a.out_scores) {
+    const uint64_t head = __shfl(v[0], 0);
+    const int start = (gmax && cnt && head == gmax) ? 1 : 0;
+    const int c = min(a.k_final, cnt - start);
+    float* sc = a.out_scores + (size_t)row * a.k_final;
+    int64_t* id = a.out_ids + (size_t)row * a.k_final;
+#pragma unroll
+    for (int s = 0; s < E; ++s) {
+      const int i = s * 64 + lane - start;
+      if (i >= 0 && i < a.k_final) {
+        sc[i] = i < c ? float_of_ord(ordk_of(v[s])) : 0.f;
+        id[i] = i < c ? (int64_t)gid_of(v[s]) : (int64_t)-1;
+      }
+    }
+    for (int i = 64 * E - start + lane; i < a.k_final; i += 64) {
+      sc[i] = 0.f;
+      id[i] = -1;
+    }
+    if (a.out_counts && lane == 0) a.out_counts[row] = c;
+    return;
+  }
+  uint64_t* out = a.keys_out + (size_t)row * a.K;
+#pragma unroll
+  for (int s = 0; s < E; ++s) {
+    const int e = s * 64 + lane;
+    if (e < a.K) out[e] = v[s];  // keys past cnt are 0
+  }
+  for (int e = 64 * E + lane; e < a.K; e += 64) out[e] = 0ull;
+}
+
+__device__ const uint32_t kWordOnes = 0xFFFFFFFFu;
+__device__ const uint32_t kWordZero = 0u;
+
+template <int ABL>
 __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   __shared__ __attribute__((aligned(16))) char dsm[kSelectLds];
   uint64_t* cand = (uint64_t*)dsm;
   uint32_t* hist = (uint32_t*)(dsm + kOffHist);
   uint32_t* tmx = (uint32_t*)(dsm + kOffTmax);
+  uint32_t* tlist = (uint32_t*)(dsm + kOffTlist);
   uint32_t* misc = (uint32_t*)(dsm + kOffMisc);  // [0..15] scalars
   uint32_t* scan_sh = misc + 16;                  // 8 words
   uint64_t* red = (uint64_t*)(misc + 32);         // 4 u64
 
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = a.n_cols, K = a.K;
   const int ntiles = (n + 31) >> 5;
   const float* Srow = a.S + (size_t)row * a.lds;
   const uint32_t* trow = a.tmax + (size_t)row * a.ldt;
+  const uint32_t* prow = a.max_inout ? a.pmax + (size_t)row * a.ldt : nullptr;
   const uint32_t* excl = a.excl ? a.excl + (size_t)row * a.excl_ld : nullptr;
   const uint64_t* carry = a.carry_in ? a.carry_in + (size_t)row * K : nullptr;
+  const int64_t w0 = a.slab_start >> 5;
 
-  auto words = [&](int tile, uint32_t& pw, uint32_t& mw, uint32_t& ew) {
-    const int64_t w = (a.slab_start >> 5) + tile;
-    pw = a.present ? a.present[w] : ~0u;
-    mw = a.mask ? a.mask[w] : ~0u;
-    ew = excl ? excl[w] : 0u;
+  // eligibility word of a tile: present ∧ mask ∧ ¬excl, three loads issued together
+  // (a null bitset reads a constant word instead of branching)
+  auto elig = [&](int tile) -> uint32_t {
+    const uint32_t* pp = a.present ? a.present + w0 + tile : &kWordOnes;
+    const uint32_t* mp = a.mask ? a.mask + w0 + tile : &kWordOnes;
+    const uint32_t* ep = excl ? excl + w0 + tile : &kWordZero;
+    return *pp & *mp & ~*ep;
   };
 
   if (tid == 0) {
     misc[6] = 0;  // T0 (atomicMax)
     misc[7] = 0;  // candidate count
-    *(uint64_t*)(misc + 10) = 0ull;  // running rank-0 key
+    misc[8] = 0;  // qualifying-tile count
+    *(uint64_t*)(misc + 10) = 0ull;  // rank-0 key of this query
   }
-  __syncthreads();
 
-  // ---- rank 0: first present item holding the largest present maximum ----
-  if (a.max_inout) {
-    const uint32_t* prow = a.pmax + (size_t)row * a.ldt;
-    uint64_t best = 0;  // (ord << 32) | ~tile : larger = higher ord, then lower tile
-    for (int t0 = tid; t0 < ntiles; t0 += 4 * kSelectThreads) {
-      uint32_t pv[4];
+  // ---- one round of loads: tile maxima (and present maxima for rank 0) ----
+  constexpr int kB = 4;
+  uint32_t v0[kB], p0[kB];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int t = t0 + b * kSelectThreads;
-        pv[b] = t < ntiles ? prow[t] : 0u;
-      }
+  for (int b = 0; b < kB; ++b) {
+    const int t = tid + b * kSelectThreads;
+    v0[b] = t < ntiles ? trow[t] : 0u;
+    p0[b] = (prow && t < ntiles) ? prow[t] : 0u;
+  }
+  uint32_t tm = 0;
+  uint64_t best = 0;  // (present max << 32) | ~tile : larger = higher ord, then lower tile
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int t = t0 + b * kSelectThreads;
-        const uint64_t v = ((uint64_t)pv[b] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)t);
-        best = (pv[b] && v > best) ? v : best;
-      }
+  for (int b = 0; b < kB; ++b) {
+    const int t = tid + b * kSelectThreads;
+    tm = v0[b] > tm ? v0[b] : tm;
+    const uint64_t pv = ((uint64_t)p0[b] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)t);
+    best = (p0[b] && pv > best) ? pv : best;
+  }
+  for (int t = tid + kB * kSelectThreads; t < ntiles; t += kSelectThreads) {  // slabs > 32K columns
+    const uint32_t v = trow[t];
+    tm = v > tm ? v : tm;
+    if (prow) {
+      const uint32_t pm = prow[t];
+      const uint64_t pv = ((uint64_t)pm << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)t);
+      best = (pm && pv > best) ? pv : best;
     }
+  }
+  tmx[tid] = tm;
+  if (prow) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const uint64_t y = __shfl_xor(best, o);
       best = y > best ? y : best;
     }
-    if (lane == 0) red[tid >> 6] = best;
-    __syncthreads();
-    if (tid < 64) {
-      uint64_t b = red[0];
-      for (int i = 1; i < kSelectThreads / 64; ++i) b = red[i] > b ? red[i] : b;
-      const uint32_t P = (uint32_t)(b >> 32);
-      uint64_t key = 0;
-      if (P) {
-        const int t = (int)(0xFFFFFFFFu - (uint32_t)b);
-        const int j = t * 32 + (lane & 31);
-        uint32_t pw, mw, ew;
-        words(t, pw, mw, ew);
-        const bool hit = lane < 32 && j < n && ((pw >> (lane & 31)) & 1u) && ord_of(Srow[j]) == P;
-        const uint64_t m = __ballot(hit);
-        if (m) key = make_key(P, a.gid0 + (uint32_t)(t * 32 + __builtin_ctzll(m)));
-      }
-      if (tid == 0) {
-        const uint64_t prev = a.first_slab ? 0ull : a.max_inout[row];
-        const uint64_t m = key > prev ? key : prev;
-        a.max_inout[row] = m;
-        *(uint64_t*)(misc + 10) = m;  // for the final-output drop below
-      }
+    if (lane == 0) red[wave] = best;
+  }
+  if constexpr (ABL == 1) { if (tm == 0x12345u) a.keys_out[row] = tm; return; }
+  __syncthreads();  // B1
+
+  // ---- rank 0 (similar / hybrid content side): wave 0 reads the winning tile now and
+  // resolves it after B2, so its latency hides behind the bound computation ----
+  uint32_t P0 = 0, r0_word = 0;
+  int r0_tile = 0;
+  float r0_val = 0.f;
+  if (prow && wave == 0) {
+    uint64_t b = red[0];
+#pragma unroll
+    for (int i = 1; i < kSelectThreads / 64; ++i) b = red[i] > b ? red[i] : b;
+    P0 = (uint32_t)(b >> 32);
+    r0_tile = (int)(0xFFFFFFFFu - (uint32_t)b);
+    if (P0 && lane < 32) {
+      const int j = r0_tile * 32 + lane;
+      r0_val = j < n ? Srow[j] : 0.f;
+      r0_word = a.present ? a.present[w0 + r0_tile] : ~0u;
     }
   }
 
   // ---- bound: T0 = K-th largest per-thread max of the tile maxima ----
-  // (loads batched kB per thread so one memory latency covers kB tiles)
-  constexpr int kB = 4;
-  uint32_t tm = 0;
-  uint32_t v0[kB];  // the first batch stays in registers for the gather below
-#pragma unroll
-  for (int b = 0; b < kB; ++b) {
-    const int t = tid + b * kSelectThreads;
-    v0[b] = t < ntiles ? trow[t] : 0u;
-    tm = v0[b] > tm ? v0[b] : tm;
-  }
-  for (int t0 = tid + kB * kSelectThreads; t0 < ntiles; t0 += kB * kSelectThreads) {
-    uint32_t v[kB];
-#pragma unroll
-    for (int b = 0; b < kB; ++b) {
-      const int t = t0 + b * kSelectThreads;
-      v[b] = t < ntiles ? trow[t] : 0u;
-    }
-#pragma unroll
-    for (int b = 0; b < kB; ++b) tm = v[b] > tm ? v[b] : tm;
-  }
-  tmx[tid] = tm;
-  __syncthreads();
   if (tm) {  // rank of my maximum among the 256 (16-B LDS reads, all independent)
     uint32_t ge = 0;
 #pragma unroll 8
@@ -315,24 +391,61 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     }
     if (ge >= (uint32_t)K) atomicMax(&misc[6], tm);
   }
-  __syncthreads();
+  __syncthreads();  // B2
   uint32_t T0 = misc[6];
   if (carry) {
     const uint32_t ck = ordk_of(carry[K - 1]);  // K carried keys are >= ck
     T0 = ck > T0 ? ck : T0;
   }
   if (T0 == 0) T0 = 1;  // fewer than K threads see eligible items: take every eligible one
+  if constexpr (ABL == 2) { if (T0 == 0x12345u) a.keys_out[row] = T0; return; }
 
-  // ---- gather: only tiles whose eligible max reaches T0 ----
-  // Qualifying tiles (~K per row) are spread over the threads; a thread issues its tile's
-  // eight 16-B score loads at once.  The first batch of tile maxima is still in registers.
+  if (prow && wave == 0) {
+    uint64_t key = 0;
+    if (P0) {
+      const bool hit = lane < 32 && r0_tile * 32 + lane < n && ((r0_word >> lane) & 1u) && ord_of(r0_val) == P0;
+      const uint64_t m = __ballot(hit);
+      if (m) key = make_key(P0, a.gid0 + (uint32_t)(r0_tile * 32 + __builtin_ctzll(m)));
+    }
+    if (lane == 0) {
+      const uint64_t prev = a.first_slab ? 0ull : a.max_inout[row];
+      const uint64_t m = key > prev ? key : prev;
+      a.max_inout[row] = m;
+      *(uint64_t*)(misc + 10) = m;  // for the final-output drop below
+    }
+  }
+
+  // ---- qualifying tiles -> compact list; carried keys -> candidates ----
+#pragma unroll
+  for (int b = 0; b < kB; ++b) {
+    const int t = tid + b * kSelectThreads;
+    if (t < ntiles && v0[b] >= T0) {
+      const uint32_t p = atomicAdd(&misc[8], 1u);
+      if (p < (uint32_t)kTileCap) tlist[p] = (uint32_t)t;
+    }
+  }
+  for (int t = tid + kB * kSelectThreads; t < ntiles; t += kSelectThreads)
+    if (trow[t] >= T0) {
+      const uint32_t p = atomicAdd(&misc[8], 1u);
+      if (p < (uint32_t)kTileCap) tlist[p] = (uint32_t)t;
+    }
+  if (carry)
+    for (int c = tid; c < K; c += kSelectThreads) {
+      const uint64_t key = carry[c];
+      if (key && ordk_of(key) >= T0) {
+        const uint32_t p = atomicAdd(&misc[7], 1u);
+        if (p < kCandCap) cand[p] = key;
+      }
+    }
+  __syncthreads();  // B3
+
+  // ---- gather: each thread takes whole qualifying tiles (one latency round when the
+  // list has <= 256 tiles): eligibility words and the tile's eight 16-B score loads ----
   auto gather_tile = [&](int t) {
-    uint32_t pw, mw, ew;
-    words(t, pw, mw, ew);
-    const uint32_t ok = pw & mw & ~ew;
     float4 v[8];
 #pragma unroll
     for (int c4 = 0; c4 < 8; ++c4) v[c4] = *(const float4*)(Srow + t * 32 + 4 * c4);
+    const uint32_t ok = elig(t);
 #pragma unroll
     for (int c4 = 0; c4 < 8; ++c4) {
       const float f[4] = {v[c4].x, v[c4].y, v[c4].z, v[c4].w};
@@ -347,45 +460,43 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
       }
     }
   };
-#pragma unroll
-  for (int b = 0; b < kB; ++b) {
-    const int t = tid + b * kSelectThreads;
-    if (t < ntiles && v0[b] >= T0) gather_tile(t);
+  const uint32_t ntl = misc[8];
+  if (ntl <= (uint32_t)kTileCap) {
+    for (uint32_t i = tid; i < ntl; i += kSelectThreads) gather_tile((int)tlist[i]);
+  } else {  // list overflow (masses of ties at the bound): every tile reaching T0
+    for (int t = tid; t < ntiles; t += kSelectThreads)
+      if (trow[t] >= T0) gather_tile(t);
   }
-  for (int t = tid + kB * kSelectThreads; t < ntiles; t += kSelectThreads)
-    if (trow[t] >= T0) gather_tile(t);
-  if (carry)
-    for (int c = tid; c < K; c += kSelectThreads) {
-      const uint64_t key = carry[c];
-      if (key && ordk_of(key) >= T0) {
-        const uint32_t p = atomicAdd(&misc[7], 1u);
-        if (p < kCandCap) cand[p] = key;
-      }
-    }
-  __syncthreads();
+  __syncthreads();  // B4
   uint32_t cnt = misc[7];
+  if constexpr (ABL == 4) { if (cnt == 0x12345u) a.keys_out[row] = cnt; return; }
   if (cnt > (uint32_t)kCandCap) {
     __syncthreads();
     auto ord_at = [&](int j) -> uint32_t {
-      uint32_t pw, mw, ew;
-      words(j >> 5, pw, mw, ew);
-      const int it = j & 31;
-      return (((pw & mw & ~ew) >> it) & 1u) ? ord_of(Srow[j]) : 0u;
+      const uint32_t ok = elig(j >> 5);
+      return ((ok >> (j & 31)) & 1u) ? ord_of(Srow[j]) : 0u;
     };
     cnt = radix_select(ord_at, n, a.gid0, carry, K, cand, hist, misc, scan_sh);
   }
+  const uint64_t gmax = *(const uint64_t*)(misc + 10);  // 0 = no rank-0 drop
 
   // ---- sort candidates by full key, emit the top K ----
+  if (cnt <= 256) {  // one wave, registers only
+    if (wave != 0) return;
+    if (cnt <= 64) wave_sort_emit<1>(cand, (int)cnt, a, row, gmax);
+    else if (cnt <= 128) wave_sort_emit<2>(cand, (int)cnt, a, row, gmax);
+    else wave_sort_emit<4>(cand, (int)cnt, a, row, gmax);
+    return;
+  }
   int P = 1;
   while (P < (int)cnt) P <<= 1;
   for (int i = (int)cnt + tid; i < P; i += kSelectThreads) cand[i] = 0ull;
   __syncthreads();
-  bitonic_desc_u64(cand, P);
+  if constexpr (ABL != 8) bitonic_desc_u64(cand, P);
   if (a.out_scores) {
     // final list of a single-list mode (semantic / similar / CF) on its last slab: drop
     // rank 0 when it is the head of the list (a present-but-masked rank 0 is not in it),
     // then emit k_final (score, id) pairs — what finalize does for one shard.
-    const uint64_t gmax = *(const uint64_t*)(misc + 10);  // set by tid 0 above (0 = no drop)
     const int start = (gmax && cnt && cand[0] == gmax) ? 1 : 0;
     const int c = min(a.k_final, (int)cnt - start);
     float* sc = a.out_scores + (size_t)row * a.k_final;
@@ -411,7 +522,14 @@ hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s) {
   if (a.K <= 0 || a.K > kMaxKInt || B <= 0 || a.n_cols <= 0 || !a.tmax || (a.max_inout && !a.pmax) ||
       (a.slab_start & 31))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(select_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
+  static const int abl = getenv("BB_SELECT_ABLATE") ? atoi(getenv("BB_SELECT_ABLATE")) : 0;
+  switch (abl) {
+    case 1: hipLaunchKernelGGL(select_kernel<1>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(select_kernel<2>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(select_kernel<4>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(select_kernel<8>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
+    default: hipLaunchKernelGGL(select_kernel<0>, dim3(B), dim3(kSelectThreads), 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -7,7 +7,7 @@
 #include <cstdio>
 #include <vector>
 
-#include "../brickbrain-rec-engine_amd/csrc/scan_kernel.h"
+#include "../brickbrain-rec-engine_amd/csrc/scan2_kernel.h"
 
 using namespace bb;
 
@@ -15,6 +15,12 @@ template <int ABL>
 void launch(const GemmArgs& a, int n_chunks, int tiles, hipStream_t s) {
   const int n_groups = a.Mpad / 128;
   hipLaunchKernelGGL((scan_kernel<float, 96, ABL>), dim3(n_groups * n_chunks), dim3(256), 0, s, a, n_chunks, tiles);
+}
+
+template <int ABL>
+void launch2(const GemmArgs& a, int n_chunks, int tiles, hipStream_t s) {
+  const int n_groups = a.Mpad / 128;
+  hipLaunchKernelGGL((scan2_kernel<float, 96, ABL>), dim3(n_groups * n_chunks), dim3(256), 0, s, a, n_chunks, tiles);
 }
 
 int main() {
@@ -44,8 +50,10 @@ int main() {
   (void)hipEventCreate(&e1);
   struct V { const char* name; void (*f)(const GemmArgs&, int, int, hipStream_t); };
   std::vector<V> vs = {{"full", launch<0>}, {"no_epilogue", launch<1>}, {"no_staging", launch<2>},
-                       {"no_barrier", launch<4>}, {"mfma_lds_only", launch<7>}};
-  for (int chunks : {128, 64, 256}) {
+                       {"no_barrier", launch<4>}, {"mfma_lds_only", launch<7>},
+                       {"v2_full", launch2<0>}, {"v2_no_epilogue", launch2<1>}, {"v2_no_staging", launch2<2>},
+                       {"v2_mfma_lds_only", launch2<7>}};
+  for (int chunks : {128}) {
     std::vector<std::vector<float>> t(vs.size());
     for (int r = 0; r < 5; ++r)
       for (size_t v = 0; v < vs.size(); ++v) {
