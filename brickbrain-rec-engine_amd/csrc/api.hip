@@ -16,6 +16,8 @@
 #include "../../include/brickrec.h"
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace bb;
 
 namespace {
@@ -457,8 +459,20 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   for (int64_t b0 = 0; b0 < B; b0 += Bc) {
     const int bc = (int)std::min<int64_t>(Bc, B - b0);
     const int bpad = (int)round_up(bc, kTileRows);
-    // ---- query prep ----
-    if (need_content) {
+    // ---- query prep: fused into the scan kernel's prologue when it runs (gathered item
+    // rows; raw f32 rows with 16-B rows), otherwise a prep launch fills qn / qcf ----
+    const bool scan_c = gemm_uses_scan(x->dtype, bpad, x->Dpad);
+    const bool scan_f = need_cf && gemm_uses_scan(x->dtype, bpad, x->Rpad);
+    const bool gather_c = q->mode != BB_MODE_SEMANTIC && d_items;
+    const float* rows_c = d_rows ? (const float*)((const char*)d_rows + (size_t)b0 * x->d * es_q) : nullptr;
+    const float* rows_f = d_cf ? (const float*)((const char*)d_cf + (size_t)b0 * x->r * es_cf) : nullptr;
+    static const bool no_fuse = getenv("BB_NO_FUSE_PREP") != nullptr;
+    const bool fuse_c = !no_fuse && need_content && scan_c &&
+                        (gather_c || (x->dtype == F32 && q->q_dtype == F32 && x->d % 4 == 0 && rows_c &&
+                                      ((uintptr_t)rows_c & 15) == 0));
+    const bool fuse_f = !no_fuse && scan_f && x->dtype == F32 && q->q_cf_dtype == F32 && x->r % 4 == 0 && rows_f &&
+                        ((uintptr_t)rows_f & 15) == 0;
+    if (need_content && !fuse_c) {
       PrepArgs pa{};
       pa.Bpad = bpad;
       pa.B = bc;
@@ -479,7 +493,7 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
       }
       if ((rc = timed(x, K_PREP, s, [&] { return launch_prep(pa, s); }))) return rc;
     }
-    if (need_cf) {
+    if (need_cf && !fuse_f) {
       PrepArgs pa{};
       pa.Bpad = bpad;
       pa.B = bc;
@@ -524,6 +538,19 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
         ga.tmax = (uint32_t*)x->tmax.p;
         ga.pmax = (uint32_t*)x->tmax.p + (size_t)Bc * ldt;
         ga.ldt = ldt;
+        if (cf_side ? fuse_f : fuse_c) {
+          ga.q_d = cf_side ? x->r : x->d;
+          if (!cf_side && gather_c) {
+            ga.q_ids = (const int64_t*)d_items + b0;
+            ga.q_id_offset = x->id_offset;
+            ga.q_n_items = x->n;
+            ga.q_items_base = x->items.p;
+          } else {
+            ga.q_src = cf_side ? rows_f : rows_c;
+            ga.q_src_ld = ga.q_d;
+            ga.q_normalize = !cf_side && q->mode == BB_MODE_SEMANTIC;
+          }
+        }
         if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(x->dtype, ga, s); }))) return rc;
         const int pp = (int)(sl & 1);
         SelectArgs sa{};

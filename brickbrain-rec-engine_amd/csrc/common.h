@@ -129,6 +129,7 @@ struct MaskArgs {
 
 // launchers (stream-ordered, no sync, no allocation)
 hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s);
+bool gemm_uses_scan(int dtype, int Mpad, int Kpad);  // the query-resident scan kernel runs
 int gemm_tile_m(int dtype);
 int gemm_tile_n(int dtype);
 int gemm_tile_k(int dtype);

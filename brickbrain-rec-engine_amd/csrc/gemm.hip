@@ -80,13 +80,18 @@ bool scan_supported(int dtype, int Kpad) {
   return ku == 8 || ku == 16 || ku == 24 || ku == 32 || ku == 48 || ku == 64 || ku == 96;
 }
 
+bool gemm_uses_scan(int dtype, int Mpad, int Kpad) {
+  return Mpad % (kScanWaves * 32) == 0 && scan_supported(dtype, Kpad) && !getenv("BB_FORCE_TILED_GEMM");
+}
+
 hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   const int bm = gemm_tile_m(dtype), bn = gemm_tile_n(dtype), bk = gemm_tile_k(dtype);
   if (a.Mpad % bm || a.Ncols % bn || a.Kpad % bk || a.Mpad <= 0 || a.Ncols <= 0 || (a.slab_start & 31))
     return hipErrorInvalidValue;
-  if (a.Mpad % (kScanWaves * 32) == 0 && scan_supported(dtype, a.Kpad) && !getenv("BB_FORCE_TILED_GEMM")) {
+  if (gemm_uses_scan(dtype, a.Mpad, a.Kpad)) {
     if (dtype == BF16 ? launch_scan<uint16_t>(a, s) : launch_scan<float>(a, s)) return hipGetLastError();
   }
+  if (a.q_ids || a.q_src) return hipErrorInvalidValue;  // the fused query prologue is scan-only
   const int blocks = (a.Mpad / bm) * (a.Ncols / bn);
   if (dtype == BF16) {
     constexpr int nt = CfgBF16::WM * CfgBF16::WN * 64;

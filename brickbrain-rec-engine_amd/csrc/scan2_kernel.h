@@ -61,23 +61,26 @@ __device__ __forceinline__ void scan2_load_queries(const GemmArgs& a, int q, int
       x[u] = k0 < d ? t : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (a.q_normalize) {
-      double ss = 0.0;
+      // f32 sum of squares (4 partial sums), as sklearn's einsum does for f32 input; a
+      // norm error only scales the whole query row, so it never reorders its items
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        ss += (double)x[u].x * x[u].x;
-        ss += (double)x[u].y * x[u].y;
-        ss += (double)x[u].z * x[u].z;
-        ss += (double)x[u].w * x[u].w;
+        s0 = fmaf(x[u].x, x[u].x, s0);
+        s1 = fmaf(x[u].y, x[u].y, s1);
+        s2 = fmaf(x[u].z, x[u].z, s2);
+        s3 = fmaf(x[u].w, x[u].w, s3);
       }
+      float ss = (s0 + s1) + (s2 + s3);
       ss += __shfl_xor(ss, 32);
-      double nrm = sqrt(ss);
-      if (nrm == 0.0) nrm = 1.0;
+      const float nrm = __fsqrt_rn(ss);
+      const float inv = nrm == 0.f ? 1.f : __fdiv_rn(1.f, nrm);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        x[u].x = (float)((double)x[u].x / nrm);
-        x[u].y = (float)((double)x[u].y / nrm);
-        x[u].z = (float)((double)x[u].z / nrm);
-        x[u].w = (float)((double)x[u].w / nrm);
+        x[u].x *= inv;
+        x[u].y *= inv;
+        x[u].z *= inv;
+        x[u].w *= inv;
       }
     }
 #pragma unroll
@@ -180,7 +183,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   __syncthreads();
   asm volatile("s_nop 4");
 
-  f32x16s accE0, accE1, accO0, accO1;
+  f32x16s accE0 = {}, accE1 = {}, accO0 = {}, accO1 = {};
   uint32_t pw = 0, mw = 0, ew = 0;     // eligibility words of the tile whose epilogue is pending
   uint32_t nw_p = 0, nw_m = 0, nw_e = 0;
 

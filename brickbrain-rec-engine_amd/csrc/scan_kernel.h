@@ -62,7 +62,6 @@ __device__ __forceinline__ void scan_epilogue(const GemmArgs& a, float* Srow, in
 // stores, 2 = no staging after the first tile, 4 = no per-tile wait + barrier.
 template <typename T, int KU, int ABL = 0>
 __global__ __launch_bounds__(kScanWaves * 64, 1) void scan_kernel(GemmArgs a, int n_chunks, int tiles_total) {
-  constexpr int NT = kScanWaves * 64;
   constexpr int ROWB = KU * 16;
   constexpr int TILE_B = 32 * ROWB;
   static_assert(ROWB <= kScanRowMax, "row too wide for the scan kernel");

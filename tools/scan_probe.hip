@@ -18,6 +18,17 @@ void launch(const GemmArgs& a, int n_chunks, int tiles, hipStream_t s) {
 }
 
 template <int ABL>
+void launch2q(const GemmArgs& a0, int n_chunks, int tiles, hipStream_t s) {
+  GemmArgs a = a0;
+  a.q_src = a.Q;
+  a.q_src_ld = a.ldq;
+  a.q_d = a.Kpad;
+  a.q_normalize = ABL == 0;
+  const int n_groups = a.Mpad / 128;
+  hipLaunchKernelGGL((scan2_kernel<float, 96, 0>), dim3(n_groups * n_chunks), dim3(256), 0, s, a, n_chunks, tiles);
+}
+
+template <int ABL>
 void launch2(const GemmArgs& a, int n_chunks, int tiles, hipStream_t s) {
   const int n_groups = a.Mpad / 128;
   hipLaunchKernelGGL((scan2_kernel<float, 96, ABL>), dim3(n_groups * n_chunks), dim3(256), 0, s, a, n_chunks, tiles);
@@ -52,7 +63,7 @@ int main() {
   std::vector<V> vs = {{"full", launch<0>}, {"no_epilogue", launch<1>}, {"no_staging", launch<2>},
                        {"no_barrier", launch<4>}, {"mfma_lds_only", launch<7>},
                        {"v2_full", launch2<0>}, {"v2_no_epilogue", launch2<1>}, {"v2_no_staging", launch2<2>},
-                       {"v2_mfma_lds_only", launch2<7>}};
+                       {"v2_mfma_lds_only", launch2<7>}, {"v2_qsrc_norm", launch2q<0>}, {"v2_qsrc_raw", launch2q<1>}};
   for (int chunks : {128}) {
     std::vector<std::vector<float>> t(vs.size());
     for (int r = 0; r < 5; ++r)
