@@ -263,22 +263,20 @@ def _suggestions(constraint: HardConstraint) -> List[str]:
 class HardConstraintFilter:
     """Drop-in for ``HardConstraintFilter`` (hard_constraint_filter.py:68-662).
 
-    ``catalog`` is the shared :class:`brickrec.catalog.Catalog` (item space, attribute
-    columns on the device); it is built from ``dbcon`` on first use when not given."""
+    ``engine`` is the shared :class:`brickrec.catalog.Engine` (catalogue + device index with
+    the attribute columns); one is built from ``dbcon`` when not given."""
 
-    def __init__(self, dbcon, catalog=None):
+    def __init__(self, dbcon, engine=None):
+        from .catalog import Engine
         self.dbcon = dbcon
-        self._catalog = catalog
+        self.engine = engine if engine is not None else Engine(dbcon)
         self._theme_cache: Dict[tuple, List[int]] = {}
         self.performance_stats = {'total_constraints_applied': 0, 'total_sets_filtered': 0,
                                   'average_filter_time_ms': 0, 'constraint_hit_rates': {}}
 
     @property
     def catalog(self):
-        if self._catalog is None:
-            from .catalog import Catalog
-            self._catalog = Catalog.from_db(self.dbcon)
-        return self._catalog
+        return self.engine.ensure_catalog()
 
     def create_constraint_set(self, **kw) -> List[HardConstraint]:
         return create_constraint_set_values(**kw)
@@ -298,7 +296,7 @@ class HardConstraintFilter:
         pred = predicate_from_constraints(constraints, cat.theme_names, owned, wished)
         if pred is None:
             return np.zeros(cat.n, dtype=bool)
-        return cat.index.eval_mask(pred)
+        return self.engine.ensure_index().eval_mask(pred)
 
     def apply_constraints(self, constraints: List[HardConstraint],
                           candidate_set_nums: Optional[List[str]] = None) -> ConstraintResult:

@@ -331,6 +331,30 @@ class ItemIndex:
                                           int(n_parts), C.byref(res)), "bb_finalize")
         return out
 
+    def get_rows(self, ids):
+        """Stored (normalised) rows of global ids: numpy in -> numpy out (f32 view of the
+        index dtype: f32, or bf16 widened), torch CUDA int64 in -> torch tensor out."""
+        if _is_torch(ids):
+            import torch
+            dt = torch.float32 if self.dtype == "f32" else torch.bfloat16
+            out = torch.empty((int(ids.shape[0]), self.d), dtype=dt, device=ids.device)
+            ids = ids.contiguous()
+            with self._mu:
+                L.check(self._lib.bb_get_rows(self._h, ids.data_ptr(), int(ids.shape[0]), out.data_ptr(),
+                                              L.BB_DEVICE), "bb_get_rows")
+            return out
+        a = np.ascontiguousarray(np.asarray(ids, np.int64))
+        if self.dtype == "f32":
+            out = np.empty((len(a), self.d), np.float32)
+        else:
+            out = np.empty((len(a), self.d), np.uint16)
+        with self._mu:
+            L.check(self._lib.bb_get_rows(self._h, a.ctypes.data, len(a), out.ctypes.data, L.BB_HOST),
+                    "bb_get_rows")
+        if self.dtype != "f32":
+            out = (out.astype(np.uint32) << 16).view(np.float32)
+        return out
+
     # ------------------------------------------------------------------ profiling
     def set_profiling(self, on: bool):
         L.check(self._lib.bb_set_profiling(self._h, int(bool(on))), "bb_set_profiling")

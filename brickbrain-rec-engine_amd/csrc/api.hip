@@ -237,6 +237,40 @@ int bb_info(bb_index* x, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* 
   return BB_OK;
 }
 
+int bb_get_rows(bb_index* x, const int64_t* ids, int32_t B, void* out, int32_t where) {
+  if (!x || !ids || !out || B <= 0) return fail(BB_E_ARG, "bb_get_rows: bad arguments");
+  if (x->n <= 0) return fail(BB_E_STATE, "no items uploaded");
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  const size_t es = elem_size(x->dtype);
+  const int bpad = (int)round_up(B, kTileRows);
+  int rc;
+  if ((rc = x->tmp.ensure((size_t)bpad * x->Dpad * es + (size_t)B * 8 + 256))) return rc;
+  char* rows = (char*)x->tmp.p;
+  const int64_t* d_ids = ids;
+  if (where != BB_DEVICE) {
+    int64_t* staged = (int64_t*)(rows + round_up((int64_t)bpad * x->Dpad * es, 256));
+    BB_HIP(hipMemcpyAsync(staged, ids, (size_t)B * 8, hipMemcpyHostToDevice, x->stream));
+    d_ids = staged;
+  }
+  PrepArgs pa{};
+  pa.Bpad = bpad;
+  pa.B = B;
+  pa.d = x->d;
+  pa.Dpad = x->Dpad;
+  pa.out = rows;
+  pa.out_dtype = x->dtype;
+  pa.items = x->items.p;
+  pa.n_items = x->n;
+  pa.id_offset = x->id_offset;
+  pa.item_ids = d_ids;
+  BB_HIP(launch_prep(pa, x->stream));
+  BB_HIP(hipMemcpy2DAsync(out, (size_t)x->d * es, rows, (size_t)x->Dpad * es, (size_t)x->d * es, B,
+                          where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, x->stream));
+  BB_HIP(hipStreamSynchronize(x->stream));
+  return BB_OK;
+}
+
 // Upload rows (host or device) in chunks through the staging buffer and convert them into
 // dst (Npad × ldst, index dtype), normalising when asked.
 static int upload_rows(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t in_dtype, int normalize,

@@ -182,6 +182,13 @@ typedef struct {
 int bb_set_profiling(bb_index* idx, int32_t on);
 int bb_get_profile(bb_index* idx, bb_profile* out);
 
+/* Stored (normalised, index-dtype) item rows of B global ids into out (B×d, row-major;
+ * ids outside this index's rows give zero rows).  ids and out live at `where`.  Lets a
+ * row-sharded deployment hand the owning shard's row of a liked set to every shard
+ * (SIMILAR / HYBRID queries with q_rows instead of q_items), the sharded analogue of
+ * feat_matrix[target_idx] (recommendation_system.py:213).  Synchronous. */
+int bb_get_rows(bb_index* idx, const int64_t* ids, int32_t B, void* out, int32_t where);
+
 int bb_info(bb_index* idx, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* r);
 int bb_destroy(bb_index* idx);
 const char* bb_last_error(void);
