@@ -42,6 +42,15 @@ from .constraints import ConstraintResult, HardConstraint, HardConstraintFilter
 logger = logging.getLogger(__name__)
 
 
+def _read_sql(sql, con, params=None):
+    """pd.read_sql on a plain DB-API connection (psycopg2, as the reference), without
+    pandas' "only SQLAlchemy is tested" warning."""
+    import warnings
+    with warnings.catch_warnings():
+        warnings.filterwarnings("ignore", message="pandas only supports SQLAlchemy")
+        return pd.read_sql(sql, con, params=params)
+
+
 def _current_year() -> int:
     """Clock used by the age score (recommendation_system.py:156); patchable in tests."""
     return datetime.now().year
@@ -128,7 +137,7 @@ class ContentBasedRecommender:
     # ---------------------------------------------------------------- features (:91-192)
     def prepare_features(self):
         logger.info("Preparing content-based features")
-        self.set_feat = pd.read_sql(_FEATURE_SQL, self.dbcon)
+        self.set_feat = _read_sql(_FEATURE_SQL, self.dbcon)
         for c in ("num_parts", "unique_parts", "unique_colors", "avg_part_quantity"):
             self.set_feat[c] = self.set_feat[c].fillna(0)
         self.set_feat["complexity_score"] = self._calculate_complexity_score()
@@ -264,7 +273,7 @@ class CollaborativeFilteringRecommender:
         ORDER BY user_id, set_num;
         """
         try:
-            ratings_df = pd.read_sql(query, self.dbcon)
+            ratings_df = _read_sql(query, self.dbcon)
             if ratings_df.empty:
                 logger.info("No user rating data found, creating synthetic data for testing")
                 ratings_df = self.synthetic_ratings
@@ -281,7 +290,7 @@ class CollaborativeFilteringRecommender:
     def _create_synthetic_user_data(self):
         """:340-366 — same global-RNG draws (seed 42) as the reference."""
         np.random.seed(42)
-        set_nums = pd.read_sql("SELECT set_num FROM sets LIMIT 100", self.dbcon)["set_num"].tolist()
+        set_nums = _read_sql("SELECT set_num FROM sets LIMIT 100", self.dbcon)["set_num"].tolist()
         data = []
         for user_id in range(1, 51):
             num_ratings = np.random.randint(10, 31)
@@ -385,7 +394,7 @@ class CollaborativeFilteringRecommender:
         """
         params.append(top_k)
         try:
-            df = pd.read_sql(q, self.dbcon, params=params)
+            df = _read_sql(q, self.dbcon, params)
             return [RecommendationResult(
                 set_num=r["set_num"], name=r["name"], score=float(r["avg_rating"]),
                 reasons=[f"Popular set with {r['rating_count']} ratings"], theme_name=r["theme_name"],
@@ -415,7 +424,7 @@ class CollaborativeFilteringRecommender:
         q += " ORDER BY s.year DESC, s.num_parts DESC LIMIT %s"
         params.append(top_k)
         try:
-            df = pd.read_sql(q, self.dbcon, params=params)
+            df = _read_sql(q, self.dbcon, params)
             return [RecommendationResult(
                 set_num=r["set_num"], name=r["name"], score=0.8, reasons=["Popular recent set"],
                 theme_name=r["theme_name"] or "Unknown", year=int(r["year"]), num_parts=int(r["num_parts"]),
@@ -540,7 +549,7 @@ class HybridRecommender:
         """
         params.append(top_k)
         try:
-            df = pd.read_sql(q, self.dbcon, params=params)
+            df = _read_sql(q, self.dbcon, params)
             out = []
             for _, r in df.iterrows():
                 reasons = ["Popular choice"]
