@@ -2,10 +2,15 @@
 
 Workload (configs[1]): batch of 256 query embeddings × 25,216 × 384-d item matrix, exact
 cosine top-50, one MI355X per rank.  A step = one bb_search over one batch with the item
-matrix and the queries already resident in HBM (prep -> MFMA score slab -> top-K select
--> finalize).  At 25K items the index does not shard: with --gpus N every
-rank serves its own batch against a full replica ("replicas only", weak scaling, no
-collective on the data path); value = queries of all ranks / max-over-ranks wall time.
+matrix and the queries already resident in HBM (MFMA scan with fused query normalisation
+-> top-K select writing the final lists).  --inflight L (default 3) keeps L batches in
+flight per GPU: L index handles on L HIP streams, steps alternating between them, so one
+batch's latency-bound select and the scan's last-tile imbalance overlap the next batch's
+scan; every step still runs its complete search.  p50_ms is the per-step latency in that
+regime, p50_ms_serial the latency of one batch alone.  At 25K items the index does not
+shard: with --gpus N every rank serves its own batches against a full
+replica ("replicas only", weak scaling, no collective on the data path); value = queries
+of all ranks / max-over-ranks wall time.
 
 Launch: python bench.py [--gpus 1 --steps 500 --warmup 50]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -84,6 +89,7 @@ def main():
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--inflight", type=int, default=3, help="batches in flight per GPU (1 = strictly serial)")
     args = ap.parse_args()
 
     import torch
@@ -99,14 +105,21 @@ def main():
     import brickrec
     B = args.batch
     x = unit_rows_torch(N_ITEMS, DIM, 1234, dev)              # replica of the item matrix
-    q = unit_rows_torch(B, DIM, 4321 + rank, dev)              # this rank's batch
-    idx = brickrec.ItemIndex(device=local, dtype=args.dtype)
-    idx.upload_items(x)
-    stream = torch.cuda.current_stream(dev)
-    run, (o_sc, o_ids, o_cnt) = idx.prepared_search("semantic", TOPK, q_rows=q, stream=stream)
+    # `inflight` batches in flight: each lane is its own index handle (own HIP stream,
+    # workspace and 39 MB item copy) serving its own batch; consecutive steps alternate
+    # lanes, so one batch's latency-bound select overlaps the next batch's MFMA scan.
+    lanes = []
+    for j in range(args.inflight):
+        q_j = unit_rows_torch(B, DIM, 4321 + rank + 1000 * j, dev)
+        idx_j = brickrec.ItemIndex(device=local, dtype=args.dtype)
+        idx_j.upload_items(x)
+        s_j = torch.cuda.current_stream(dev) if args.inflight == 1 else torch.cuda.Stream(dev)
+        run_j, outs_j = idx_j.prepared_search("semantic", TOPK, q_rows=q_j, stream=s_j)
+        lanes.append((idx_j, s_j, run_j, outs_j, q_j))
+    idx, stream, run, (o_sc, o_ids, o_cnt), q = lanes[0]
 
-    for _ in range(args.warmup):
-        run()
+    for i in range(args.warmup):
+        lanes[i % len(lanes)][2]()
     torch.cuda.synchronize()
 
     # ---- timed region: K steps, barrier + sync on both sides, max over ranks ----
@@ -116,9 +129,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
-        run()
-        ev[i][1].record(stream)
+        _, s_i, run_i, _, _ = lanes[i % len(lanes)]
+        ev[i][0].record(s_i)
+        run_i()
+        ev[i][1].record(s_i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -128,6 +142,17 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
+
+    # ---- single-batch latency without other batches in flight (lane 0 alone) ----
+    ser = []
+    for _ in range(min(args.steps, 200)):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        run()
+        b.record(stream)
+        ser.append((a, b))
+    torch.cuda.synchronize()
+    lat_serial = np.array([a.elapsed_time(b) for a, b in ser])
 
     # ---- per-kernel device time (HIP events on the launch stream), same K steps ----
     idx.set_profiling(True)
@@ -148,7 +173,8 @@ def main():
     flush = torch.empty(640 << 20, dtype=torch.uint8, device=dev)
     cold = []
     for i in range(20):
-        flush.fill_(i & 0xFF)
+        with torch.cuda.stream(stream):
+            flush.fill_(i & 0xFF)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         run()
@@ -166,6 +192,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * el / args.steps, 4),
         "p50_ms": round(float(np.median(lat_ms)), 4),
+        "p50_ms_serial": round(float(np.median(lat_serial)), 4),
         "p50_ms_mall_cold": round(float(np.median(cold)), 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -174,7 +201,8 @@ def main():
         "data": "synthetic (unit-norm N(0,1) rows, seeds 1234 / 4321+rank)",
         "config": {"workload": "configs[1]: batch=256 queries x 25,216 x 384-d items, cosine top-50",
                    "items": N_ITEMS, "dim": DIM, "batch": B, "top_k": TOPK,
-                   "parallelism": f"replicas x{world}" if world > 1 else "single"},
+                   "parallelism": f"replicas x{world}" if world > 1 else "single",
+                   "inflight_batches": args.inflight},
         "roofline": {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
                      "frac": round(achieved / peak, 4), "traffic": hbm,
                      "kernel": KERNEL[args.dtype] if not os.environ.get("BB_FORCE_TILED_GEMM") else "gemm_nt_kernel",

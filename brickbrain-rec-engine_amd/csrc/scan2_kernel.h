@@ -94,8 +94,39 @@ __device__ __forceinline__ void scan2_load_queries(const GemmArgs& a, int q, int
   for (int u = 0; u < U; ++u) qf[u] = *(const uint4*)(qrow + (2 * u + h) * 16);
 }
 
+// Per-lane half-tile maxima of one 32-item tile (this lane's 16 items): te over eligible
+// items (present ∧ mask ∧ ¬excl, in range), tp over present in-range items, as order
+// images.  Fast path (wave-uniform): every item of the tile is eligible for every query
+// of the wave — a float max3 tree, then one order image (+0.0f folds -0 into +0, so the
+// bound stays >= every element's image); otherwise a per-item masked scan.
+__device__ __forceinline__ void tile_maxima(const f32x16s& p, int tile0, int n_valid, uint32_t pw, uint32_t ok, int h,
+                                            uint32_t& te, uint32_t& tp) {
+  if (__all(tile0 + 32 <= n_valid && pw == 0xFFFFFFFFu && ok == 0xFFFFFFFFu)) {
+    const float m0 = fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3]));
+    const float m1 = fmaxf(fmaxf(p[4], p[5]), fmaxf(p[6], p[7]));
+    const float m2 = fmaxf(fmaxf(p[8], p[9]), fmaxf(p[10], p[11]));
+    const float m3 = fmaxf(fmaxf(p[12], p[13]), fmaxf(p[14], p[15]));
+    te = tp = ord_of(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)) + 0.0f);
+    return;
+  }
+  uint32_t e = 0, t = 0;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int it = (g & 3) + 8 * (g >> 2) + 4 * h;
+    const uint32_t o = ord_of(p[g]);
+    const bool in = tile0 + it < n_valid;
+    const uint32_t op = (in && ((pw >> it) & 1u)) ? o : 0u;
+    const uint32_t oe = (in && ((ok >> it) & 1u)) ? o : 0u;
+    t = op > t ? op : t;
+    e = oe > e ? oe : e;
+  }
+  te = e;
+  tp = t;
+}
+
 // ABL (tools/scan_probe only): 1 = no epilogue, 2 = no staging after the first tile,
-// 4 = no per-tile wait + barrier.
+// 4 = no per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no
+// order-image / maxima arithmetic.
 template <typename T, int KU, int ABL = 0>
 __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, int n_chunks, int tiles_total) {
   constexpr int U = KU / 2;               // u-steps per tile (16-B chunk pairs)
@@ -183,23 +214,22 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   __syncthreads();
   asm volatile("s_nop 4");
 
-  f32x16s accE0 = {}, accE1 = {}, accO0 = {}, accO1 = {};
+  f32x16s accE = {}, accO = {};
   uint32_t pw = 0, mw = 0, ew = 0;     // eligibility words of the tile whose epilogue is pending
   uint32_t nw_p = 0, nw_m = 0, nw_e = 0;
 
-  // One tile: MFMA chain over LDS buffer BUF into (c0, c1); interleaved: the epilogue of the
-  // previous tile held in (p0, p1) (EPI), this tile's eligibility words, the next tile's
-  // staging into BUF^1.
-  constexpr int kEpiSlices = 15 + PIECES;
-  auto tile_body = [&](auto BUF, auto EPI, int tile, f32x16s& c0, f32x16s& c1, const f32x16s& p0,
-                       const f32x16s& p1) __attribute__((always_inline)) {
+  // One tile: ONE accumulation chain (back-to-back dependent MFMAs run at full rate) over
+  // LDS buffer BUF into c; woven in: the previous tile's epilogue on p (EPI), this tile's
+  // eligibility words, the next tile's staging into BUF^1.  On the f32 MFMA, VALU work does
+  // NOT overlap (it holds the SIMD's vector issue), so the epilogue is kept to ~25 VALU in
+  // the common all-eligible case (tile_maxima fast path).
+  constexpr int kEpiSlices = 8 + PIECES;
+  auto tile_body = [&](auto BUF, auto EPI, int tile, f32x16s& c, const f32x16s& p) __attribute__((always_inline)) {
     constexpr int buf = decltype(BUF)::value;
     constexpr bool epi = decltype(EPI)::value && !(ABL & 1);
     const int ptile = tile - 1;
     const int stile = tile + 1 < tile_hi ? tile + 1 : tile;  // branch-free staging target
-    float v[16];
     uint32_t te = 0, tp = 0;
-    const uint32_t ok = pw & mw & ~ew;
     const int ptile0 = ptile * 32;
     // item fragments: ds_read issued two u-steps ahead of their MFMAs
     auto frag = [&](int u) __attribute__((always_inline)) {
@@ -213,68 +243,52 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
       if constexpr (u + 2 < U) fq[(u + 2) % 3] = frag(u + 2);
       const uint4 fa = fq[u % 3];
       // MFMAs as inline asm so the resident query operand stays in AGPRs (srcB may be an
-      // AGPR on gfx950); the VGPR file is left to the fragments and the woven epilogue.
+      // AGPR on gfx950) and the accumulator in VGPRs (read by the epilogue without copies).
       if constexpr (sizeof(T) == 4) {
         const float pa[4] = {__uint_as_float(fa.x), __uint_as_float(fa.y), __uint_as_float(fa.z),
                              __uint_as_float(fa.w)};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          f32x16s& acc = (u & 1) ? c1 : c0;
-          if (u < 2 && c == 0)
-            asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, 0" : "=a"(acc) : "v"(pa[c]), "a"(qa[4 * u + c]));
+        for (int cc = 0; cc < 4; ++cc) {
+          if (u == 0 && cc == 0)
+            asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, 0" : "=v"(c) : "v"(pa[cc]), "a"(qa[4 * u + cc]));
           else
-            asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(pa[c]), "a"(qa[4 * u + c]));
+            asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, %0" : "+v"(c) : "v"(pa[cc]), "a"(qa[4 * u + cc]));
         }
       } else {
-        f32x16s& acc = (u & 1) ? c1 : c0;
         const u32x4v fv = __builtin_bit_cast(u32x4v, fa);
-        if constexpr (u < 2)
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(fv), "a"(qv[u]));
+        if constexpr (u == 0)
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(c) : "v"(fv), "a"(qv[u]));
         else
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(fv), "a"(qv[u]));
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[u]));
       }
       // ---- slices scheduled on this u-step: slice s runs at u = min(U-1, s+2) ----
       static_for<kEpiSlices>([&](auto SS) {
         constexpr int s = decltype(SS)::value;
         constexpr int su = (s + 2 < U) ? s + 2 : U - 1;
         if constexpr (su == u) {
-          if constexpr (s < 8) {
-            if constexpr (epi) {
-#pragma unroll
-              for (int e = 0; e < 2; ++e) {
-                const int g = 2 * s + e;
-                v[g] = p0[g] + p1[g];
-                const int it = (g & 3) + 8 * (g >> 2) + 4 * h;
-                const uint32_t o = ord_of(v[g]);
-                const bool in = ptile0 + it < a.n_valid;
-                const uint32_t op = (in && ((pw >> it) & 1u)) ? o : 0u;
-                const uint32_t oe = (in && ((ok >> it) & 1u)) ? o : 0u;
-                tp = op > tp ? op : tp;
-                te = oe > te ? oe : te;
-              }
-            }
-          } else if constexpr (s == 8) {
-            if constexpr (epi) {
-              const uint32_t te2 = __shfl_xor(te, 32), tp2 = __shfl_xor(tp, 32);
+          if constexpr (s == 0) {
+            if constexpr (epi && !(ABL & 32)) tile_maxima(p, ptile0, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
+          } else if constexpr (s == 1) {
+            if constexpr (epi && !(ABL & 32)) {
+              const uint32_t te2 = xor32(te), tp2 = xor32(tp);
               te = te2 > te ? te2 : te;
               tp = tp2 > tp ? tp2 : tp;
             }
-          } else if constexpr (s < 13) {
-            if constexpr (epi) {
-              constexpr int j = s - 9;
-              *(float4*)(Srow + ptile0 + 8 * j + 4 * h) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+          } else if constexpr (s < 6) {
+            if constexpr (epi && !(ABL & 8)) {
+              constexpr int j = s - 2;
+              *(float4*)(Srow + ptile0 + 8 * j + 4 * h) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
             }
-          } else if constexpr (s == 13) {
-            if constexpr (epi) {
-              a.tmax[(size_t)q * a.ldt + ptile] = te;
-              a.pmax[(size_t)q * a.ldt + ptile] = tp;
+          } else if constexpr (s == 6) {
+            if constexpr (epi && !(ABL & 16)) {
+              (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
             }
-          } else if constexpr (s == 14) {
+          } else if constexpr (s == 7) {
             nw_p = a.present[w0 + tile];
             nw_m = a.mask[w0 + tile];
             nw_e = erow[w0 + tile];
           } else {
-            if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s - 15);
+            if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s - 8);
           }
         }
       });
@@ -289,32 +303,37 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   };
 
   // final epilogue of the last tile (not overlapped)
-  auto last_epilogue = [&](int tile, const f32x16s& p0, const f32x16s& p1) __attribute__((always_inline)) {
+  auto last_epilogue = [&](int tile, const f32x16s& p) __attribute__((always_inline)) {
     if constexpr (ABL & 1) return;
-    float v[16];
+    uint32_t te = 0, tp = 0;
+    tile_maxima(p, tile * 32, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
+    const uint32_t te2 = xor32(te), tp2 = xor32(tp);
+    te = te2 > te ? te2 : te;
+    tp = tp2 > tp ? tp2 : tp;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) v[g] = p0[g] + p1[g];
-    scan_epilogue(a, Srow, q, h, tile, v, pw, mw, ew);
+    for (int j = 0; j < 4; ++j)
+      *(float4*)(Srow + tile * 32 + 8 * j + 4 * h) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+    (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
   };
 
   using B0 = std::integral_constant<int, 0>;
   using B1 = std::integral_constant<int, 1>;
   using EY = std::integral_constant<bool, true>;
   using EN = std::integral_constant<bool, false>;
-  tile_body(B0{}, EN{}, tile_lo, accE0, accE1, accO0, accO1);
+  tile_body(B0{}, EN{}, tile_lo, accE, accO);
   int tile = tile_lo + 1;
   for (;;) {
     if (tile >= tile_hi) {
-      last_epilogue(tile - 1, accE0, accE1);
+      last_epilogue(tile - 1, accE);
       break;
     }
-    tile_body(B1{}, EY{}, tile, accO0, accO1, accE0, accE1);
+    tile_body(B1{}, EY{}, tile, accO, accE);
     ++tile;
     if (tile >= tile_hi) {
-      last_epilogue(tile - 1, accO0, accO1);
+      last_epilogue(tile - 1, accO);
       break;
     }
-    tile_body(B0{}, EY{}, tile, accE0, accE1, accO0, accO1);
+    tile_body(B0{}, EY{}, tile, accE, accO);
     ++tile;
   }
 }

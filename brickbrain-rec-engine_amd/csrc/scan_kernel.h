@@ -29,6 +29,13 @@ __device__ __forceinline__ int scan_swz(int r) {
   return (KU % 16 == 0) ? (r & 15) : (r & 7);
 }
 
+// x of lane (l ^ 32): one v_permlane32_swap (gfx950), no LDS round trip — a ds_bpermute
+// here would make the next s_waitcnt lgkmcnt drain the MFMA fragment prefetch queue.
+__device__ __forceinline__ uint32_t xor32(uint32_t x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (threadIdx.x & 32) ? r[0] : r[1];
+}
+
 // Epilogue of one 32-item tile for this lane's query: 16-B row segments of S and the
 // tile maxima over eligible (present ∧ mask ∧ ¬excl) and present items.  Branch-free:
 // both lane halves hold the combined maxima and store the same word.
@@ -50,11 +57,11 @@ __device__ __forceinline__ void scan_epilogue(const GemmArgs& a, float* Srow, in
     tp = op > tp ? op : tp;
     te = oe > te ? oe : te;
   }
-  const uint32_t te2 = __shfl_xor(te, 32), tp2 = __shfl_xor(tp, 32);
+  const uint32_t te2 = xor32(te), tp2 = xor32(tp);
   te = te2 > te ? te2 : te;
   tp = tp2 > tp ? tp2 : tp;
-  a.tmax[(size_t)q * a.ldt + tile] = te;
-  a.pmax[(size_t)q * a.ldt + tile] = tp;
+  // one store instruction: the lower half writes tmax, the upper half pmax
+  (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
 }
 
 // KU = Kpad·sizeof(T)/16: 16-byte chunks per row (f32: 4 k-steps each; bf16: 1 MFMA each).

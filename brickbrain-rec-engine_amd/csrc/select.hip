@@ -403,9 +403,13 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   if (prow && wave == 0) {
     uint64_t key = 0;
     if (P0) {
-      const bool hit = lane < 32 && r0_tile * 32 + lane < n && ((r0_word >> lane) & 1u) && ord_of(r0_val) == P0;
+      // float compare: the maxima fold -0 into +0, and numpy's argmax treats them as equal
+      const bool hit = lane < 32 && r0_tile * 32 + lane < n && ((r0_word >> lane) & 1u) && r0_val == float_of_ord(P0);
       const uint64_t m = __ballot(hit);
-      if (m) key = make_key(P0, a.gid0 + (uint32_t)(r0_tile * 32 + __builtin_ctzll(m)));
+      if (m) {
+        const int j0 = (int)__builtin_ctzll(m);
+        key = make_key(ord_of(__shfl(r0_val, j0)), a.gid0 + (uint32_t)(r0_tile * 32 + j0));
+      }
     }
     if (lane == 0) {
       const uint64_t prev = a.first_slab ? 0ull : a.max_inout[row];

@@ -63,7 +63,9 @@ int main() {
   std::vector<V> vs = {{"full", launch<0>}, {"no_epilogue", launch<1>}, {"no_staging", launch<2>},
                        {"no_barrier", launch<4>}, {"mfma_lds_only", launch<7>},
                        {"v2_full", launch2<0>}, {"v2_no_epilogue", launch2<1>}, {"v2_no_staging", launch2<2>},
-                       {"v2_mfma_lds_only", launch2<7>}, {"v2_qsrc_norm", launch2q<0>}, {"v2_qsrc_raw", launch2q<1>}};
+                       {"v2_mfma_lds_only", launch2<7>}, {"v2_qsrc_norm", launch2q<0>}, {"v2_qsrc_raw", launch2q<1>},
+                       {"v2_no_S", launch2<8>}, {"v2_no_max", launch2<16 | 32>}, {"v2_no_maxstore", launch2<16>},
+                       {"v2_only_accread", launch2<8 | 16 | 32>}};
   for (int chunks : {128}) {
     std::vector<std::vector<float>> t(vs.size());
     for (int r = 0; r < 5; ++r)
