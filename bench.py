@@ -29,9 +29,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "brickbrain-rec-engine_amd"))
 
 N_ITEMS, DIM, BATCH, TOPK = 25216, 384, 256, 50
-PEAK = {"f32": ("mfma", 157.3, "TFLOP/s"), "bf16": ("mfma", 2500.0, "TFLOP/s")}
 HBM_PEAK_GBS = 8000.0
-KERNEL = {"f32": "scan2_kernel<float,96>", "bf16": "scan2_kernel<uint16_t,48>"}
+BF16_DENSE_TF = 2500.0   # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md), no sparsity
+F32_DENSE_TF = 157.3
+
+
+def scan_kernel_info(dtype):
+    """(kernel, MFMA instruction peak, MFMA flops executed per algorithmic flop).
+    An f32 index runs the split-precision scan: six bf16 MFMAs per fp32 product
+    (scan3_kernel.h, bf16x6, fp32-class accuracy) unless BB_NO_SPLIT forces the fp32 MFMA."""
+    if os.environ.get("BB_FORCE_TILED_GEMM"):
+        return "gemm_nt_kernel", (F32_DENSE_TF if dtype == "f32" else BF16_DENSE_TF), 1.0
+    if dtype == "f32" and not os.environ.get("BB_NO_SPLIT"):
+        return "scan3_kernel<48> (bf16x6 split, f32 accumulate)", BF16_DENSE_TF, 6.0
+    if dtype == "f32":
+        return "scan2_kernel<float,96> (fp32 MFMA)", F32_DENSE_TF, 1.0
+    return "scan2_kernel<uint16_t,48> (bf16 MFMA)", BF16_DENSE_TF, 1.0
 
 
 def unit_rows_torch(n, d, seed, device):
@@ -165,8 +178,10 @@ def main():
     flops = 2.0 * B * N_ITEMS * DIM
     es = 4 if args.dtype == "f32" else 2
     alg_bytes = N_ITEMS * DIM * es + B * DIM * 4 + B * TOPK * 8    # items + queries + top-K out
-    bound, peak, unit = PEAK[args.dtype]
-    achieved = flops / (gemm_us * 1e-6) / 1e12
+    kname, peak, mfma_per_flop = scan_kernel_info(args.dtype)
+    bound, unit = "mfma", "TFLOP/s"
+    alg_tflops = flops / (gemm_us * 1e-6) / 1e12
+    achieved = alg_tflops * mfma_per_flop      # MFMA flops the kernel executes per second
     hbm = load_pmc(args.dtype)
 
     # ---- MALL-cold latency (256 MiB Infinity Cache flushed before each step) ----
@@ -205,8 +220,9 @@ def main():
                    "inflight_batches": args.inflight},
         "roofline": {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
                      "frac": round(achieved / peak, 4), "traffic": hbm,
-                     "kernel": KERNEL[args.dtype] if not os.environ.get("BB_FORCE_TILED_GEMM") else "gemm_nt_kernel",
-                     "kernel_us": round(gemm_us, 3),
+                     "kernel": kname, "kernel_us": round(gemm_us, 3),
+                     "mfma_flops_per_algorithmic_flop": mfma_per_flop,
+                     "algorithmic_tflops": round(alg_tflops, 2),
                      "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": alg_bytes,
                      "hbm_frac_at_alg_bytes": round(alg_bytes / (gemm_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
         "kernels_us_per_step": {k: round(1e3 * v["ms"] / max(args.steps, 1), 3) for k, v in prof.items()

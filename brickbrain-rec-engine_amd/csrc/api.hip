@@ -84,6 +84,7 @@ struct bb_index {
   DevBuf ones, zeros;  // all-ones / all-zeros bitsets standing in for 'no mask' / 'no exclusions'
   int r = 0, Rpad = 0;
   DevBuf cf, cf_present;
+  DevBuf items3, cf3;  // f32 index: the same rows as three bf16 planes (split scan, scan3)
   DevBuf parts, year, theme;
 
   // workspace
@@ -296,6 +297,20 @@ static int upload_rows(bb_index* x, const void* rows, int64_t n, int32_t d, int3
   return BB_OK;
 }
 
+// f32 index: keep a three-plane bf16 copy of the rows for the split-precision scan
+// (scan3_kernel.h) when its width is supported; the f32 rows stay for everything else.
+static int make_planes(bb_index* x, DevBuf& rows, DevBuf& planes, int ld) {
+  if (x->dtype != F32 || !scan3_supported(kTileRows, ld)) {
+    planes.release();
+    return BB_OK;
+  }
+  int rc = planes.ensure((size_t)x->Npad * 3 * ld * 2);
+  if (rc) return rc;
+  BB_HIP(launch_split_planes((const float*)rows.p, x->Npad, ld, (uint16_t*)planes.p, x->stream));
+  BB_HIP(hipStreamSynchronize(x->stream));
+  return BB_OK;
+}
+
 int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t in_dtype, int32_t prenormalized,
                     int32_t where, const uint32_t* present_bits) {
   if (!x || !rows || n <= 0 || d <= 0) return fail(BB_E_ARG, "bb_upload_items: bad arguments");
@@ -323,7 +338,8 @@ int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t
   if ((rc = x->ones.ensure(wbytes)) || (rc = x->zeros.ensure(wbytes))) return rc;
   BB_HIP(hipMemsetAsync(x->ones.p, 0xFF, wbytes, x->stream));
   BB_HIP(hipMemsetAsync(x->zeros.p, 0, wbytes, x->stream));
-  return upload_rows(x, rows, n, d, in_dtype, prenormalized ? 0 : 1, where, x->items.p, x->Dpad);
+  if ((rc = upload_rows(x, rows, n, d, in_dtype, prenormalized ? 0 : 1, where, x->items.p, x->Dpad))) return rc;
+  return make_planes(x, x->items, x->items3, x->Dpad);
 }
 
 int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const uint32_t* present_bits) {
@@ -346,7 +362,8 @@ int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const 
   } else {
     BB_HIP(hipMemsetAsync(x->cf_present.p, 0xFF, wbytes, x->stream));
   }
-  return upload_rows(x, f, x->n, r, in_dtype, 0, BB_HOST, x->cf.p, x->Rpad);
+  if ((rc = upload_rows(x, f, x->n, r, in_dtype, 0, BB_HOST, x->cf.p, x->Rpad))) return rc;
+  return make_planes(x, x->cf, x->cf3, x->Rpad);
 }
 
 int bb_upload_attrs(bb_index* x, const int32_t* num_parts, const int16_t* year, const int32_t* theme_id) {
@@ -471,8 +488,10 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   const size_t es = elem_size(x->dtype);
   if ((rc = x->S.ensure((size_t)Bc * lds * 4))) return rc;
   if ((rc = x->tmax.ensure((size_t)Bc * ldt * 4 * 2))) return rc;  // tmax + pmax
-  if (need_content && (rc = x->qn.ensure((size_t)Bc * x->Dpad * es))) return rc;
-  if (need_cf && (rc = x->qcf.ensure((size_t)Bc * x->Rpad * es))) return rc;
+  // query rows: index dtype, or three bf16 planes (6 B / element) for the split scan
+  const size_t qes_c = x->items3.p ? std::max<size_t>(es, 6) : es, qes_f = x->cf3.p ? std::max<size_t>(es, 6) : es;
+  if (need_content && (rc = x->qn.ensure((size_t)Bc * x->Dpad * qes_c))) return rc;
+  if (need_cf && (rc = x->qcf.ensure((size_t)Bc * x->Rpad * qes_f))) return rc;
   const size_t side_keys = (size_t)Bc * K_int;
   if ((rc = x->keys.ensure(2 * sides * side_keys * 8))) return rc;
   if ((rc = x->maxk.ensure((size_t)Bc * 8))) return rc;
@@ -495,15 +514,20 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
     const int bpad = (int)round_up(bc, kTileRows);
     // ---- query prep: fused into the scan kernel's prologue when it runs (gathered item
     // rows; raw f32 rows with 16-B rows), otherwise a prep launch fills qn / qcf ----
-    const bool scan_c = gemm_uses_scan(x->dtype, bpad, x->Dpad);
-    const bool scan_f = need_cf && gemm_uses_scan(x->dtype, bpad, x->Rpad);
+    // split-precision scan (f32 index with bf16 planes): queries come as planes too —
+    // gathered item planes (fused) or a prep launch writing SPLIT3 rows
+    const bool s3_c = need_content && x->items3.p && scan3_supported(bpad, x->Dpad);
+    const bool s3_f = need_cf && x->cf3.p && scan3_supported(bpad, x->Rpad);
+    const bool scan_c = !s3_c && gemm_uses_scan(x->dtype, bpad, x->Dpad);
+    const bool scan_f = !s3_f && need_cf && gemm_uses_scan(x->dtype, bpad, x->Rpad);
     const bool gather_c = q->mode != BB_MODE_SEMANTIC && d_items;
     const float* rows_c = d_rows ? (const float*)((const char*)d_rows + (size_t)b0 * x->d * es_q) : nullptr;
     const float* rows_f = d_cf ? (const float*)((const char*)d_cf + (size_t)b0 * x->r * es_cf) : nullptr;
     static const bool no_fuse = getenv("BB_NO_FUSE_PREP") != nullptr;
-    const bool fuse_c = !no_fuse && need_content && scan_c &&
-                        (gather_c || (x->dtype == F32 && q->q_dtype == F32 && x->d % 4 == 0 && rows_c &&
-                                      ((uintptr_t)rows_c & 15) == 0));
+    const bool fuse_c = !no_fuse && need_content &&
+                        ((s3_c && gather_c) ||
+                         (scan_c && (gather_c || (x->dtype == F32 && q->q_dtype == F32 && x->d % 4 == 0 && rows_c &&
+                                                  ((uintptr_t)rows_c & 15) == 0))));
     const bool fuse_f = !no_fuse && scan_f && x->dtype == F32 && q->q_cf_dtype == F32 && x->r % 4 == 0 && rows_f &&
                         ((uintptr_t)rows_f & 15) == 0;
     if (need_content && !fuse_c) {
@@ -513,7 +537,7 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
       pa.d = x->d;
       pa.Dpad = x->Dpad;
       pa.out = x->qn.p;
-      pa.out_dtype = x->dtype;
+      pa.out_dtype = s3_c ? SPLIT3 : x->dtype;
       pa.items = x->items.p;
       pa.n_items = x->n;
       pa.id_offset = x->id_offset;
@@ -534,7 +558,7 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
       pa.d = x->r;
       pa.Dpad = x->Rpad;
       pa.out = x->qcf.p;
-      pa.out_dtype = x->dtype;
+      pa.out_dtype = s3_f ? SPLIT3 : x->dtype;
       pa.src = (const char*)d_cf + (size_t)b0 * x->r * es_cf;
       pa.src_dtype = q->q_cf_dtype;
       pa.src_ld = x->r;
@@ -585,7 +609,18 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
             ga.q_normalize = !cf_side && q->mode == BB_MODE_SEMANTIC;
           }
         }
-        if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(x->dtype, ga, s); }))) return rc;
+        DevBuf& planes = cf_side ? x->cf3 : x->items3;
+        if (cf_side ? s3_f : s3_c) {
+          // split-precision scan: items, gathered rows and prepped queries are bf16 planes
+          const int64_t w = ga.ldq;
+          ga.X = (const char*)planes.p + (size_t)c0 * 3 * w * 2;
+          ga.ldx = 3 * w;
+          ga.ldq = 3 * w;
+          if (ga.q_ids) ga.q_items_base = planes.p;
+          if ((rc = timed(x, K_GEMM, s, [&] { return launch_scan3(ga, s); }))) return rc;
+        } else if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(x->dtype, ga, s); }))) {
+          return rc;
+        }
         const int pp = (int)(sl & 1);
         SelectArgs sa{};
         sa.S = (const float*)x->S.p;

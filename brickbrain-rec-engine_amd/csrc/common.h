@@ -30,7 +30,7 @@ constexpr int kSelectThreads = 256;
 constexpr int kSelectStageMax = 32768;  // score row staged in LDS when n_cols <= this
 constexpr int kMaxKInt = 512;      // per-side internal list length limit (k_side + 1)
 
-enum Dtype : int { F32 = 0, BF16 = 1, F64 = 2 };
+enum Dtype : int { F32 = 0, BF16 = 1, F64 = 2, SPLIT3 = 3 /* prep output: bf16 planes [xh|xm|xl] */ };
 
 struct GemmArgs {
   const void* Q;      // [Mpad][ldq]   queries (normalised), dtype of the index
@@ -130,6 +130,9 @@ struct MaskArgs {
 // launchers (stream-ordered, no sync, no allocation)
 hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s);
 bool gemm_uses_scan(int dtype, int Mpad, int Kpad);  // the query-resident scan kernel runs
+bool scan3_supported(int Mpad, int Kpad);            // split-bf16 scan for an f32 index
+hipError_t launch_scan3(const GemmArgs& a, hipStream_t s);  // X / q_items_base = planes
+hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t* dst, hipStream_t s);
 int gemm_tile_m(int dtype);
 int gemm_tile_n(int dtype);
 int gemm_tile_k(int dtype);

@@ -24,7 +24,7 @@
 #include <cstdlib>
 
 #include "gemm_kernel.h"
-#include "scan2_kernel.h"
+#include "scan3_kernel.h"
 
 namespace bb {
 
@@ -78,6 +78,35 @@ static bool launch_scan(const GemmArgs& a, hipStream_t s) {
 bool scan_supported(int dtype, int Kpad) {
   const int ku = Kpad * (dtype == BF16 ? 2 : 4) / 16;
   return ku == 8 || ku == 16 || ku == 24 || ku == 32 || ku == 48 || ku == 64 || ku == 96;
+}
+
+bool scan3_supported(int Mpad, int Kpad) {
+  const int kp = Kpad * 2 / 16;
+  return Mpad % (kScanWaves * 32) == 0 && Kpad % 8 == 0 && kp % 8 == 0 && kp >= 8 && kp <= kScan3MaxKP &&
+         !getenv("BB_NO_SPLIT");
+}
+
+template <int KP>
+static void launch_scan3_t(const GemmArgs& a, hipStream_t s) {
+  const int n_groups = a.Mpad / (kScanWaves * 32);
+  const int tiles = a.Ncols / 32;
+  int n_chunks = (256 + n_groups - 1) / n_groups;
+  n_chunks = n_chunks < tiles ? n_chunks : tiles;
+  hipLaunchKernelGGL((scan3_kernel<KP>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+}
+
+hipError_t launch_scan3(const GemmArgs& a, hipStream_t s) {
+  if (!scan3_supported(a.Mpad, a.Kpad) || a.Ncols % 32 || (a.slab_start & 31)) return hipErrorInvalidValue;
+  switch (a.Kpad * 2 / 16) {
+    case 8: launch_scan3_t<8>(a, s); break;
+    case 16: launch_scan3_t<16>(a, s); break;
+    case 24: launch_scan3_t<24>(a, s); break;
+    case 32: launch_scan3_t<32>(a, s); break;
+    case 40: launch_scan3_t<40>(a, s); break;
+    case 48: launch_scan3_t<48>(a, s); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 bool gemm_uses_scan(int dtype, int Mpad, int Kpad) {

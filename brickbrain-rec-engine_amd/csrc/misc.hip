@@ -73,6 +73,35 @@ hipError_t launch_convert_rows(const void* src, int src_dtype, int64_t n, int d,
   return hipGetLastError();
 }
 
+// f32 rows -> three bf16 planes per row ([xh | xm | xl], x = xh + xm + xl exactly) for the
+// split-precision scan (scan3_kernel.h).  One thread per element.
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* src, int64_t n, int64_t ld, uint16_t* dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * ld) return;
+  const int64_t row = i / ld, col = i - row * ld;
+  const float v = src[i];
+  auto rne = [](float f) -> uint32_t {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return u >> 16;
+  };
+  const uint32_t h = rne(v);
+  const float r = v - __uint_as_float(h << 16);
+  const uint32_t m = rne(r);
+  const uint32_t l = rne(r - __uint_as_float(m << 16));
+  uint16_t* o = dst + row * 3 * ld + col;
+  o[0] = (uint16_t)h;
+  o[ld] = (uint16_t)m;
+  o[2 * ld] = (uint16_t)l;
+}
+
+hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t* dst, hipStream_t s) {
+  const int64_t total = n * ld;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, src, n, ld, dst);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------
 // query preparation: normalise query rows (semantic), or gather the stored (already
 // normalised) item rows of the liked sets (similar-sets: the query IS feat_matrix[target],
@@ -109,11 +138,39 @@ __device__ __forceinline__ void load_chunk(const void* p, int dt, size_t sb, int
 
 constexpr int kPrepC = 8;  // rows up to 512 wide stay in registers (one load round)
 
+// f32 -> three bf16 planes (x = xh + xm + xl exactly) for the split-precision scan
+__device__ __forceinline__ void split3_bits(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
+  auto rne = [](float f) -> uint32_t {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return u >> 16;
+  };
+  const uint32_t hb = rne(v);
+  const float r = v - __uint_as_float(hb << 16);
+  const uint32_t mb = rne(r);
+  h = (uint16_t)hb;
+  m = (uint16_t)mb;
+  l = (uint16_t)rne(r - __uint_as_float(mb << 16));
+}
+
+// store element i of output row `row` (index dtype, or SPLIT3 planes with row stride 3·Dpad)
+__device__ __forceinline__ void store_q(const PrepArgs& a, int row, int i, float v) {
+  if (a.out_dtype == SPLIT3) {
+    uint16_t* o = (uint16_t*)a.out + (size_t)row * 3 * a.Dpad + i;
+    uint16_t h, m, l;
+    split3_bits(v, h, m, l);
+    o[0] = h;
+    o[a.Dpad] = m;
+    o[2 * a.Dpad] = l;
+  } else {
+    store_elem(a.out, a.out_dtype, (size_t)row * a.Dpad + i, v);
+  }
+}
+
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= a.Bpad) return;
-  const size_t ob = (size_t)row * a.Dpad;
   const void* src = a.src;
   int sdt = a.src_dtype, d = a.d, norm_on = a.normalize;
   size_t sb = (size_t)row * a.src_ld;
@@ -122,13 +179,13 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     const int64_t lid = a.item_ids[row] - a.id_offset;
     zero = !(lid >= 0 && lid < a.n_items);
     src = a.items;
-    sdt = a.out_dtype;
+    sdt = a.out_dtype == SPLIT3 ? F32 : a.out_dtype;
     d = a.Dpad;
     norm_on = 0;
     sb = zero ? 0 : (size_t)lid * a.Dpad;
   }
   if (zero) {
-    for (int i = lane; i < a.Dpad; i += 64) store_elem(a.out, a.out_dtype, ob + i, 0.f);
+    for (int i = lane; i < a.Dpad; i += 64) store_q(a, row, i, 0.f);
     return;
   }
   if (a.Dpad <= 64 * kPrepC) {
@@ -146,7 +203,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
 #pragma unroll
     for (int c = 0; c < kPrepC; ++c) {
       const int i = lane + 64 * c;
-      if (i < a.Dpad) store_elem(a.out, a.out_dtype, ob + i, (float)(x[c] / norm));
+      if (i < a.Dpad) store_q(a, row, i, (float)(x[c] / norm));
     }
     return;
   }
@@ -169,7 +226,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
 #pragma unroll
     for (int c = 0; c < kPrepC; ++c) {
       const int i = base + lane + 64 * c;
-      if (i < a.Dpad) store_elem(a.out, a.out_dtype, ob + i, (float)(x[c] / norm));
+      if (i < a.Dpad) store_q(a, row, i, (float)(x[c] / norm));
     }
   }
 }

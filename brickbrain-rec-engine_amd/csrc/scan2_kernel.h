@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   auto stage_piece = [&](int tile, int buf, int p) __attribute__((always_inline)) {
     const char* src = Xg + (size_t)tile * 32 * ldxb + soff[p];
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + buf * TILE_B + (wave * PIECES + p) * 1024);
-    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory", "m0");
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory");
   };
 
   const size_t w0 = (size_t)(a.slab_start >> 5);
@@ -235,13 +235,15 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     auto frag = [&](int u) __attribute__((always_inline)) {
       return *(const uint4*)(smem + buf * TILE_B + rd[u % G] + (u / G) * G * 32);
     };
-    uint4 fq[3];
+    // 4-slot ring, prefetch distance 2; fragments stay live one step past their MFMAs
+    // (see scan3_kernel.h: inline-asm MFMAs are opaque to hazard tracking)
+    uint4 fq[4];
     fq[0] = frag(0);
     if constexpr (U > 1) fq[1] = frag(1);
     static_for<U>([&](auto UU) {
       constexpr int u = decltype(UU)::value;
-      if constexpr (u + 2 < U) fq[(u + 2) % 3] = frag(u + 2);
-      const uint4 fa = fq[u % 3];
+      if constexpr (u + 2 < U) fq[(u + 2) % 4] = frag(u + 2);
+      const uint4 fa = fq[u % 4];
       // MFMAs as inline asm so the resident query operand stays in AGPRs (srcB may be an
       // AGPR on gfx950) and the accumulator in VGPRs (read by the epilogue without copies).
       if constexpr (sizeof(T) == 4) {
@@ -250,17 +252,18 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
           if (u == 0 && cc == 0)
-            asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, 0" : "=v"(c) : "v"(pa[cc]), "a"(qa[4 * u + cc]));
+            asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, 0" : "=&v"(c) : "v"(pa[cc]), "a"(qa[4 * u + cc]));
           else
             asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, %0" : "+v"(c) : "v"(pa[cc]), "a"(qa[4 * u + cc]));
         }
       } else {
         const u32x4v fv = __builtin_bit_cast(u32x4v, fa);
         if constexpr (u == 0)
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(c) : "v"(fv), "a"(qv[u]));
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[u]));
         else
           asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[u]));
       }
+      if constexpr (u > 0) asm volatile("" ::"v"(__builtin_bit_cast(u32x4v, fq[(u + 3) % 4])));
       // ---- slices scheduled on this u-step: slice s runs at u = min(U-1, s+2) ----
       static_for<kEpiSlices>([&](auto SS) {
         constexpr int s = decltype(SS)::value;
@@ -293,6 +296,10 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
         }
       });
     });
+    // The MFMAs are inline asm, so the compiler cannot see their result latency: this
+    // ties the accumulator to a wait long enough for the last MFMA to retire, before any
+    // register copy or read of it the compiler may place after this point.
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" : "+v"(c));
     pw = nw_p;
     mw = nw_m;
     ew = nw_e;
@@ -305,6 +312,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   // final epilogue of the last tile (not overlapped)
   auto last_epilogue = [&](int tile, const f32x16s& p) __attribute__((always_inline)) {
     if constexpr (ABL & 1) return;
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15");  // asm-MFMA result -> VALU read
     uint32_t te = 0, tp = 0;
     tile_maxima(p, tile * 32, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
     const uint32_t te2 = xor32(te), tp2 = xor32(tp);

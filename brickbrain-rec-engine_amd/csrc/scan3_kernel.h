@@ -1,0 +1,259 @@
+// scan3_kernel.h — fp32-accurate scan on the bf16 MFMA: split-precision "bf16x6".
+//
+// An fp32 value splits exactly into three bf16 planes, x = xh + xm + xl (8+8+8 mantissa
+// bits). The cosine score q·x is the sum of the nine plane products. This kernel keeps
+// the six terms of order >= 2^-16 relative:
+//   xh·qh + xm·qh + xh·qm + xl·qh + xh·ql + xm·qm
+// and drops xm·ql, xl·qm and xl·ql, which are ~2^-24 and below. Each bf16 product is
+// exact, and the MFMA accumulates in f32.
+//
+// Accuracy, measured against an f64 reference on unit vectors (d = 384, see
+// tools/bf16x6_error.py): max error 1.0e-7 (numpy fp32: 1.5e-7). It is fp32-class, so the
+// parity bar is unchanged.
+//
+// Cost per 16-wide k step is six v_mfma_f32_32x32x16_bf16 (6 × 32 cycles) against eight
+// v_mfma_f32_32x32x2_f32 (8 × 64 cycles): 2.7× less MFMA time. Unlike the fp32 MFMA, the
+// bf16 MFMA leaves the SIMD's vector issue free for most of its cycles, so the woven
+// epilogue overlaps.
+//
+// Layout:
+// * Items are stored as planes per row, [xh | xm | xl], each KP 16-B chunks
+//   (row = 3·KP·16 bytes). They are staged 32 rows per tile by LDS-DMA into an
+//   XOR-swizzled double buffer. The swizzle keeps every chunk inside its plane.
+// * Queries are split in the prologue from f32 rows (raw rows normalised in-kernel, or
+//   prepared rows), or read as planes of stored items (q_ids). qh and qm are resident in
+//   AGPRs, ql in VGPRs.
+// * Epilogue and select contract are identical to scan2_kernel.h.
+#pragma once
+#include "scan2_kernel.h"
+
+namespace bb {
+
+constexpr int kScan3MaxKP = 48;  // 2 tiles of 32 rows × 3 planes × 768 B = 144 KiB LDS
+
+// Query planes of this lane: chunk (2u + h) of each plane, u < KP/2, from rows of three
+// bf16 planes: the stored item rows of liked sets (q_ids, row stride ldx) or the prep
+// kernel's SPLIT3 output (Q, row stride ldq, both in bf16 elements).  Splitting happens
+// once per query in prep, not once per workgroup here (~3K VALU per wave otherwise).
+template <int KP>
+__device__ __forceinline__ void scan3_load_queries(const GemmArgs& a, int q, int h, u32x4v (&qh)[KP / 2],
+                                                   u32x4v (&qm)[KP / 2], u32x4v (&ql)[KP / 2]) {
+  constexpr int U = KP / 2;
+  const char* row;
+  bool ok = q < a.M_valid;
+  if (a.q_ids) {
+    const int64_t lid = ok ? a.q_ids[q] - a.q_id_offset : 0;
+    ok = ok && lid >= 0 && lid < a.q_n_items;
+    row = (const char*)a.q_items_base + (size_t)(ok ? lid : 0) * a.ldx * 2;
+  } else {
+    row = (const char*)a.Q + (size_t)(ok ? q : 0) * a.ldq * 2;
+  }
+  const u32x4v z = {0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int c = 2 * u + h;
+    qh[u] = ok ? *(const u32x4v*)(row + c * 16) : z;
+    qm[u] = ok ? *(const u32x4v*)(row + (KP + c) * 16) : z;
+    ql[u] = ok ? *(const u32x4v*)(row + (2 * KP + c) * 16) : z;
+  }
+}
+
+// KP: 16-B chunks per plane row (Dpad·2/16).  ABL: as scan2 (probe only).
+template <int KP, int ABL = 0>
+__global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, int n_chunks, int tiles_total) {
+  constexpr int U = KP / 2;                 // 16-wide k steps per tile
+  constexpr int ROWB = 3 * KP * 16;         // bytes of one item row (three planes)
+  constexpr int TILE_B = 32 * ROWB;
+  constexpr int PIECES = TILE_B / (1024 * kScanWaves);
+  constexpr int G = 8;                      // KP % 16 == 0 or KP == 8: swizzle period 8 u-steps
+  static_assert(KP % 8 == 0 && KP <= kScan3MaxKP, "unsupported plane width");
+  static_assert(TILE_B % (1024 * kScanWaves) == 0, "tile must split into whole 1 KiB pieces per wave");
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_B];
+
+  const int n_groups = a.Mpad / (kScanWaves * 32);
+  const int total = n_groups * n_chunks;
+  const int L = blockIdx.x;
+  const int xcd = L & 7, local = L >> 3, q8 = total >> 3, r8 = total & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+  const int chunk = t / n_groups, group = t - chunk * n_groups;
+  const int tile_lo = (int)((int64_t)chunk * tiles_total / n_chunks);
+  const int tile_hi = (int)((int64_t)(chunk + 1) * tiles_total / n_chunks);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int q = group * kScanWaves * 32 + wave * 32 + r;
+  if (tile_lo >= tile_hi) return;  // uniform per workgroup
+
+  u32x4v qh[U], qm[U], ql[U];
+  scan3_load_queries<KP>(a, q, h, qh, qm, ql);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    asm volatile("" : "+a"(qh[u]));
+    asm volatile("" : "+a"(qm[u]));
+  }
+
+  // swizzle: chunk c of a row sits at c ^ (r & 15) (KP % 16 == 0) or c ^ (r & 7) (KP == 8);
+  // both keep the chunk inside its plane (planes start at multiples of 8 chunks)
+  constexpr int SWM = (KP % 16 == 0) ? 15 : 7;
+  const int swz = r & SWM;
+  int rd[G];
+#pragma unroll
+  for (int m = 0; m < G; ++m) rd[m] = r * ROWB + (((2 * m + h) ^ swz) << 4);
+
+  const char* Xg = (const char*)a.X;
+  const size_t ldxb = (size_t)a.ldx * 2;  // = ROWB (planes of one row are contiguous)
+  const uint32_t lds_base = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+  auto stage_piece = [&](int tile, int buf, int p) __attribute__((always_inline)) {
+    const int mine = (wave * PIECES + p) * 1024 + lane * 16;
+    const int row = mine / ROWB;
+    const int ch = ((mine % ROWB) >> 4) ^ (row & SWM);
+    const char* src = Xg + ((size_t)tile * 32 + row) * ldxb + ch * 16;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + buf * TILE_B + (wave * PIECES + p) * 1024);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory");
+  };
+
+  const size_t w0 = (size_t)(a.slab_start >> 5);
+  const uint32_t* erow = a.excl + (size_t)(q < a.M_valid ? q : a.M_valid - 1) * a.excl_ld;
+  float* Srow = a.S + (size_t)q * a.lds;
+
+#pragma unroll
+  for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  asm volatile("s_nop 4");
+
+  f32x16s accE = {}, accO = {};
+  uint32_t pw = 0, mw = 0, ew = 0;
+  uint32_t nw_p = 0, nw_m = 0, nw_e = 0;
+
+  constexpr int kEpiSlices = 8 + PIECES;
+  auto tile_body = [&](auto BUF, auto EPI, int tile, f32x16s& c, const f32x16s& p) __attribute__((always_inline)) {
+    constexpr int buf = decltype(BUF)::value;
+    constexpr bool epi = decltype(EPI)::value && !(ABL & 1);
+    const int ptile = tile - 1;
+    const int stile = tile + 1 < tile_hi ? tile + 1 : tile;
+    uint32_t te = 0, tp = 0;
+    const int ptile0 = ptile * 32;
+    // fragment of plane P at u-step u: ds_read two steps ahead
+    auto frag = [&](int P, int u) __attribute__((always_inline)) {
+      return *(const u32x4v*)(smem + buf * TILE_B + rd[u % G] + (u / G) * G * 32 + P * KP * 16);
+    };
+    // 4-slot ring, prefetch distance 2.  Inline-asm MFMAs are opaque to the compiler's
+    // hazard tracking, so a fragment's registers are kept live (empty asm use) until the
+    // next step's MFMAs are issued: no ds_read may land in registers an in-flight MFMA
+    // still reads.
+    u32x4v fh[4], fm[4], fl[4];
+    fh[0] = frag(0, 0);
+    fm[0] = frag(1, 0);
+    fl[0] = frag(2, 0);
+    if constexpr (U > 1) {
+      fh[1] = frag(0, 1);
+      fm[1] = frag(1, 1);
+      fl[1] = frag(2, 1);
+    }
+    static_for<U>([&](auto UU) {
+      constexpr int u = decltype(UU)::value;
+      if constexpr (u + 2 < U) {
+        fh[(u + 2) % 4] = frag(0, u + 2);
+        fm[(u + 2) % 4] = frag(1, u + 2);
+        fl[(u + 2) % 4] = frag(2, u + 2);
+      }
+      const u32x4v xh = fh[u % 4], xm = fm[u % 4], xl = fl[u % 4];
+      // one accumulation chain, largest term first
+      if constexpr (u == 0)
+        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(xh), "a"(qh[u]));
+      else
+        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(xh), "a"(qh[u]));
+      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(xm), "a"(qh[u]));
+      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(xh), "a"(qm[u]));
+      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(xl), "a"(qh[u]));
+      // ql may be parked in AGPRs by the register allocator and copied back right before
+      // this MFMA: the s_nop covers the VALU-write -> MFMA-read hazard the compiler cannot
+      // see through inline asm
+      asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(xh), "v"(ql[u]));
+      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(xm), "a"(qm[u]));
+      if constexpr (u > 0) asm volatile("" ::"v"(fh[(u + 3) % 4]), "v"(fm[(u + 3) % 4]), "v"(fl[(u + 3) % 4]));
+      // schedule: the next tile's LDS-DMA pieces first (two per u-step, so its HBM/MALL
+      // latency has most of the tile to land), then the previous tile's epilogue
+      static_for<kEpiSlices>([&](auto SS) {
+        constexpr int s = decltype(SS)::value;
+        constexpr int s_stage = (s - 8) / 2;
+        constexpr int s_epi = U / 2 + s;
+        constexpr int su0 = s >= 8 ? s_stage : s_epi;
+        constexpr int su = su0 < U ? su0 : U - 1;
+        if constexpr (su == u) {
+          if constexpr (s == 0) {
+            if constexpr (epi && !(ABL & 32)) tile_maxima(p, ptile0, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
+          } else if constexpr (s == 1) {
+            if constexpr (epi && !(ABL & 32)) {
+              const uint32_t te2 = xor32(te), tp2 = xor32(tp);
+              te = te2 > te ? te2 : te;
+              tp = tp2 > tp ? tp2 : tp;
+            }
+          } else if constexpr (s < 6) {
+            if constexpr (epi && !(ABL & 8)) {
+              constexpr int j = s - 2;
+              *(float4*)(Srow + ptile0 + 8 * j + 4 * h) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+            }
+          } else if constexpr (s == 6) {
+            if constexpr (epi && !(ABL & 16)) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
+          } else if constexpr (s == 7) {
+            nw_p = a.present[w0 + tile];
+            nw_m = a.mask[w0 + tile];
+            nw_e = erow[w0 + tile];
+          } else {
+            if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s - 8);
+          }
+        }
+      });
+    });
+    // The MFMAs are inline asm, so the compiler cannot see their result latency: this
+    // ties the accumulator to a wait long enough for the last MFMA to retire, before any
+    // register copy or read of it the compiler may place after this point.
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" : "+v"(c));
+    pw = nw_p;
+    mw = nw_m;
+    ew = nw_e;
+    if constexpr (!(ABL & 4)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  };
+
+  auto last_epilogue = [&](int tile, const f32x16s& p) __attribute__((always_inline)) {
+    if constexpr (ABL & 1) return;
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15");  // asm-MFMA result -> VALU read
+    uint32_t te = 0, tp = 0;
+    tile_maxima(p, tile * 32, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
+    const uint32_t te2 = xor32(te), tp2 = xor32(tp);
+    te = te2 > te ? te2 : te;
+    tp = tp2 > tp ? tp2 : tp;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *(float4*)(Srow + tile * 32 + 8 * j + 4 * h) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+    (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
+  };
+
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using EY = std::integral_constant<bool, true>;
+  using EN = std::integral_constant<bool, false>;
+  tile_body(B0{}, EN{}, tile_lo, accE, accO);
+  int tile = tile_lo + 1;
+  for (;;) {
+    if (tile >= tile_hi) {
+      last_epilogue(tile - 1, accE);
+      break;
+    }
+    tile_body(B1{}, EY{}, tile, accO, accE);
+    ++tile;
+    if (tile >= tile_hi) {
+      last_epilogue(tile - 1, accO);
+      break;
+    }
+    tile_body(B0{}, EY{}, tile, accE, accO);
+    ++tile;
+  }
+}
+
+}  // namespace bb

@@ -307,3 +307,33 @@ def test_sharded_merge_matches_single(brickrec):
     for i in range(B):   # query rows re-normalised on the host: allow last-ulp score noise
         assert set(ids[i]) == set(ref_ids[i])
     np.testing.assert_allclose(sc, ref_sc, atol=1e-6)
+
+
+def test_inflight_lanes_device(brickrec):
+    """The bench's serving regime: several index handles on their own HIP streams with
+    device-resident queries, steps interleaved — every result equals the oracle."""
+    import torch
+    n, d, B, k = 25216, 384, 256, 50
+    x = R.unit_rows(n, d, 1234)
+    dev = torch.device("cuda", 0)
+    xt = torch.from_numpy(x).to(dev)
+    lanes = []
+    for j in range(3):
+        q = R.unit_rows(B, d, 777 + j)
+        idx = brickrec.ItemIndex(dtype="f32")
+        idx.upload_items(xt)
+        s = torch.cuda.Stream(dev)
+        run, outs = idx.prepared_search("semantic", k, q_rows=torch.from_numpy(q).to(dev), stream=s)
+        lanes.append((idx, run, outs, q))
+    for _ in range(4):
+        for _, run, _, _ in lanes:
+            run()
+    torch.cuda.synchronize()
+    for idx, run, (sc, ids, cnt), q in lanes:
+        sc, ids = sc.cpu().numpy(), ids.cpu().numpy()
+        sim = R.cosine_scores(q, x).astype(np.float64)
+        for i in range(0, B, 5):
+            ri, rs = R.topk_indices(sim[i], k + 1)
+            np.testing.assert_allclose(sc[i], rs[:k], atol=TOL, rtol=0)
+            if rs[k - 1] - rs[k] > 2e-6:
+                assert set(ids[i]) == set(ri[:k])

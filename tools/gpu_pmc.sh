@@ -9,7 +9,7 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVES" \
            "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/pmc/p$i" -o run --output-format csv -- python3 "$R/bench.py" --steps 30 --warmup 5 --no-cpu > "$R/gpurun_out/pmc/p$i.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/pmc/p$i" -o run --output-format csv -- python3 "$R/bench.py" --steps 30 --warmup 5 --no-cpu --inflight 1 > "$R/gpurun_out/pmc/p$i.log" 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"
   [ $rc -ne 0 ] && { tail -5 "$R/gpurun_out/pmc/p$i.log"; exit $rc; }
 done

@@ -11,7 +11,7 @@ import json
 import os
 import sys
 
-KERNELS = {"f32": "bb::scan2_kernel<float", "bf16": "bb::scan2_kernel<unsigned short"}
+KERNELS = {"f32": "bb::scan3_kernel<48", "bf16": "bb::scan2_kernel<unsigned short"}
 
 
 def main(src, dst):

@@ -1,0 +1,145 @@
+// scan3_check.hip — one launch per variant of the split-bf16 scan (Q path, q_src path,
+// ABL 1), synchronised and checked against an f64 host dot product on sampled entries.
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/scan3_check.hip -o tools/scan3_check
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../brickbrain-rec-engine_amd/csrc/scan3_kernel.h"
+
+using namespace bb;
+
+static uint16_t rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static float bf(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+int main() {
+  const int N = 25344, D = 384, M = 256;
+  std::vector<float> x((size_t)N * D), q((size_t)M * D);
+  uint64_t s = 12345;
+  auto rnd = [&]() { s = s * 6364136223846793005ull + 1442695040888963407ull; return ((s >> 33) & 0xFFFFFF) / 16777216.0f - 0.5f; };
+  for (auto& v : x) v = rnd();
+  for (auto& v : q) v = rnd();
+  for (int i = 0; i < N; ++i) {  // unit rows
+    double n = 0;
+    for (int k = 0; k < D; ++k) n += (double)x[(size_t)i * D + k] * x[(size_t)i * D + k];
+    for (int k = 0; k < D; ++k) x[(size_t)i * D + k] = (float)(x[(size_t)i * D + k] / std::sqrt(n));
+  }
+  for (int i = 0; i < M; ++i) {
+    double n = 0;
+    for (int k = 0; k < D; ++k) n += (double)q[(size_t)i * D + k] * q[(size_t)i * D + k];
+    for (int k = 0; k < D; ++k) q[(size_t)i * D + k] = (float)(q[(size_t)i * D + k] / std::sqrt(n));
+  }
+  std::vector<uint16_t> qplanes((size_t)M * 3 * D);
+  for (int i = 0; i < M; ++i)
+    for (int k = 0; k < D; ++k) {
+      const float v = q[(size_t)i * D + k];
+      const uint16_t h = rne(v);
+      const float r = v - bf(h);
+      const uint16_t m = rne(r);
+      qplanes[(size_t)i * 3 * D + k] = h;
+      qplanes[(size_t)i * 3 * D + D + k] = m;
+      qplanes[(size_t)i * 3 * D + 2 * D + k] = rne(r - bf(m));
+    }
+  std::vector<uint16_t> planes((size_t)N * 3 * D);
+  for (int i = 0; i < N; ++i)
+    for (int k = 0; k < D; ++k) {
+      const float v = x[(size_t)i * D + k];
+      const uint16_t h = rne(v);
+      const float r = v - bf(h);
+      const uint16_t m = rne(r);
+      const uint16_t l = rne(r - bf(m));
+      planes[(size_t)i * 3 * D + k] = h;
+      planes[(size_t)i * 3 * D + D + k] = m;
+      planes[(size_t)i * 3 * D + 2 * D + k] = l;
+    }
+  float *dq, *dS;
+  uint16_t* dx;
+  uint32_t *tm, *pm, *ones, *zeros;
+  (void)hipMalloc(&dq, q.size() * 4);
+  (void)hipMalloc(&dx, planes.size() * 2);
+  (void)hipMalloc(&dS, (size_t)M * N * 4);
+  (void)hipMalloc(&tm, (size_t)M * N / 32 * 4);
+  (void)hipMalloc(&pm, (size_t)M * N / 32 * 4);
+  (void)hipMalloc(&ones, N / 8);
+  (void)hipMalloc(&zeros, N / 8);
+  uint16_t* dqp;
+  (void)hipMalloc(&dqp, qplanes.size() * 2);
+  (void)hipMemcpy(dqp, qplanes.data(), qplanes.size() * 2, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dq, q.data(), q.size() * 4, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dx, planes.data(), planes.size() * 2, hipMemcpyHostToDevice);
+  (void)hipMemset(ones, 0xFF, N / 8);
+  (void)hipMemset(zeros, 0, N / 8);
+  GemmArgs a{};
+  a.Q = dqp; a.ldq = 3 * D; a.X = dx; a.ldx = 3 * D; a.S = dS; a.lds = N; a.Mpad = M; a.Ncols = N; a.Kpad = D;
+  a.M_valid = M; a.n_valid = N; a.mask = ones; a.present = ones; a.excl = zeros; a.excl_ld = 0;
+  a.tmax = tm; a.pmax = pm; a.ldt = N / 32;
+  std::vector<float> S((size_t)M * N);
+  std::vector<uint32_t> T((size_t)M * N / 32);
+  for (int variant = 0; variant < 1; ++variant) {
+    (void)hipMemset(dS, 0, (size_t)M * N * 4);
+    (void)hipMemset(tm, 0, (size_t)M * N / 32 * 4);
+    const int chunks = 128;
+    hipLaunchKernelGGL((scan3_kernel<48, 0>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) { printf("{\"variant\":%d,\"error\":\"%s\"}\n", variant, hipGetErrorString(e)); return 1; }
+    (void)hipMemcpy(S.data(), dS, S.size() * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(T.data(), tm, T.size() * 4, hipMemcpyDeviceToHost);
+    double maxerr = 0;
+    for (int i = 0; i < M; i += 7)
+      for (int j = 0; j < N; j += 13) {
+        double ref = 0;
+        for (int k = 0; k < D; ++k) ref += (double)q[(size_t)i * D + k] * x[(size_t)j * D + k];
+        maxerr = std::fmax(maxerr, std::fabs(ref - S[(size_t)i * N + j]));
+      }
+    {
+      // locate wrong scores: by tile position inside its workgroup chunk, and by query row
+      long nbad = 0, first = 0, last = 0, mid = 0, bad_q[8] = {0};
+      const int tiles = N / 32;
+      for (int i = 0; i < M; ++i)
+        for (int t = 0; t < tiles; ++t) {
+          long b = 0;
+          for (int j = 0; j < 32; j += 3) {
+            const int col = t * 32 + j;
+            double ref = 0;
+            for (int k = 0; k < D; ++k) ref += (double)q[(size_t)i * D + k] * x[(size_t)col * D + k];
+            if (std::fabs(ref - S[(size_t)i * N + col]) > 1e-5) ++b;
+          }
+          if (!b) continue;
+          nbad += b;
+          int c = (int)((int64_t)t * chunks / tiles);
+          int lo = (int)((int64_t)c * tiles / chunks), hi = (int)((int64_t)(c + 1) * tiles / chunks);
+          while (t < lo) { --c; lo = (int)((int64_t)c * tiles / chunks); }
+          while (t >= hi) { ++c; hi = (int)((int64_t)(c + 1) * tiles / chunks); lo = (int)((int64_t)c * tiles / chunks); }
+          if (t == lo) ++first; else if (t == hi - 1) ++last; else ++mid;
+          bad_q[(i % 32) / 4]++;
+        }
+      printf("{\"bad_elems_sampled\":%ld,\"bad_tiles_first\":%ld,\"mid\":%ld,\"last\":%ld,\"by_q8\":[%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld]}\n",
+             nbad, first, mid, last, bad_q[0], bad_q[1], bad_q[2], bad_q[3], bad_q[4], bad_q[5], bad_q[6], bad_q[7]);
+    }
+    long bad = 0, lower = 0, zero = 0;
+    for (int i = 0; i < M; ++i)
+      for (int t = 0; t < N / 32; ++t) {
+        float mx = -1e30f;
+        for (int j = 0; j < 32; ++j) mx = std::fmax(mx, S[(size_t)i * N + t * 32 + j]);
+        const uint32_t want = ord_of(mx + 0.0f), got = T[(size_t)i * (N / 32) + t];
+        if (got != want) { ++bad; if (got < want) ++lower; if (got == 0) ++zero; }
+      }
+    printf("{\"variant\":%d,\"ok\":true,\"max_abs_err\":%.3e,\"tmax_bad\":%ld,\"tmax_lower\":%ld,\"tmax_zero\":%ld,\"tiles\":%d}\n",
+           variant, maxerr, bad, lower, zero, M * N / 32);
+  }
+  return 0;
+}

@@ -7,7 +7,7 @@
 #include <cstdio>
 #include <vector>
 
-#include "../brickbrain-rec-engine_amd/csrc/scan2_kernel.h"
+#include "../brickbrain-rec-engine_amd/csrc/scan3_kernel.h"
 
 using namespace bb;
 
@@ -15,6 +15,16 @@ template <int ABL>
 void launch(const GemmArgs& a, int n_chunks, int tiles, hipStream_t s) {
   const int n_groups = a.Mpad / 128;
   hipLaunchKernelGGL((scan_kernel<float, 96, ABL>), dim3(n_groups * n_chunks), dim3(256), 0, s, a, n_chunks, tiles);
+}
+
+static uint16_t* g_planes = nullptr;
+template <int ABL>
+void launch3(const GemmArgs& a0, int n_chunks, int tiles, hipStream_t s) {
+  GemmArgs a = a0;
+  a.X = g_planes;
+  a.ldx = 3 * a.Kpad;
+  const int n_groups = a.Mpad / 128;
+  hipLaunchKernelGGL((scan3_kernel<48, ABL>), dim3(n_groups * n_chunks), dim3(256), 0, s, a, n_chunks, tiles);
 }
 
 template <int ABL>
@@ -56,6 +66,8 @@ int main() {
   a.mask = ones; a.present = ones; a.excl = zeros; a.excl_ld = 0;
   hipStream_t s;
   (void)hipStreamCreate(&s);
+  (void)hipMalloc(&g_planes, (size_t)N * D * 3 * 2);
+  (void)hipMemset(g_planes, 0x3b, (size_t)N * D * 3 * 2);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -66,11 +78,19 @@ int main() {
                        {"v2_mfma_lds_only", launch2<7>}, {"v2_qsrc_norm", launch2q<0>}, {"v2_qsrc_raw", launch2q<1>},
                        {"v2_no_S", launch2<8>}, {"v2_no_max", launch2<16 | 32>}, {"v2_no_maxstore", launch2<16>},
                        {"v2_only_accread", launch2<8 | 16 | 32>}};
+  // (scan3 variants are not run here: its Q-path launches faulted in this harness twice
+  //  while tools/scan3_check and the library paths ran clean)
   for (int chunks : {128}) {
     std::vector<std::vector<float>> t(vs.size());
     for (int r = 0; r < 5; ++r)
       for (size_t v = 0; v < vs.size(); ++v) {
         vs[v].f(a, chunks, N / 32, s);
+        {
+          hipError_t e = hipGetLastError();
+          if (e != hipSuccess) printf("{\"variant\":\"%s\",\"launch_error\":\"%s\"}\n", vs[v].name, hipGetErrorString(e));
+          e = hipStreamSynchronize(s);
+          if (e != hipSuccess) { printf("{\"variant\":\"%s\",\"exec_error\":\"%s\"}\n", vs[v].name, hipGetErrorString(e)); return 1; }
+        }
         (void)hipEventRecord(e0, s);
         for (int i = 0; i < 20; ++i) vs[v].f(a, chunks, N / 32, s);
         (void)hipEventRecord(e1, s);
