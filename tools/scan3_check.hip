@@ -141,5 +141,29 @@ int main() {
     printf("{\"variant\":%d,\"ok\":true,\"max_abs_err\":%.3e,\"tmax_bad\":%ld,\"tmax_lower\":%ld,\"tmax_zero\":%ld,\"tiles\":%d}\n",
            variant, maxerr, bad, lower, zero, M * N / 32);
   }
+  // timing of ablation variants (20 launches each, after one synchronised check launch)
+  auto timeit = [&](const char* name, auto launch) {
+    launch();
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) { printf("{\"timing\":\"%s\",\"error\":\"%s\"}\n", name, hipGetErrorString(e)); return false; }
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < 20; ++i) launch();
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("{\"timing\":\"%s\",\"us\":%.2f}\n", name, ms * 1e3 / 20);
+    return true;
+  };
+  const int chunks = 128;
+  if (!timeit("full", [&] { hipLaunchKernelGGL((scan3_kernel<48, 0>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32); })) return 1;
+  if (!timeit("no_epilogue", [&] { hipLaunchKernelGGL((scan3_kernel<48, 1>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32); })) return 1;
+  if (!timeit("no_staging", [&] { hipLaunchKernelGGL((scan3_kernel<48, 2>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32); })) return 1;
+  if (!timeit("no_barrier", [&] { hipLaunchKernelGGL((scan3_kernel<48, 4>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32); })) return 1;
+  if (!timeit("mfma_lds_only", [&] { hipLaunchKernelGGL((scan3_kernel<48, 7>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32); })) return 1;
   return 0;
 }
