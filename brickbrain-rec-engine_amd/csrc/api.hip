@@ -514,8 +514,8 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
     const int bpad = (int)round_up(bc, kTileRows);
     // ---- query prep: fused into the scan kernel's prologue when it runs (gathered item
     // rows; raw f32 rows with 16-B rows), otherwise a prep launch fills qn / qcf ----
-    // split-precision scan (f32 index with bf16 planes): queries come as planes too —
-    // gathered item planes (fused) or a prep launch writing SPLIT3 rows
+    // split-precision scan (f32 index with bf16 planes): queries always come from a prep
+    // launch writing the q3f plane image (coalesced query loads in the scan)
     const bool s3_c = need_content && x->items3.p && scan3_supported(bpad, x->Dpad);
     const bool s3_f = need_cf && x->cf3.p && scan3_supported(bpad, x->Rpad);
     const bool scan_c = !s3_c && gemm_uses_scan(x->dtype, bpad, x->Dpad);
@@ -524,10 +524,9 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
     const float* rows_c = d_rows ? (const float*)((const char*)d_rows + (size_t)b0 * x->d * es_q) : nullptr;
     const float* rows_f = d_cf ? (const float*)((const char*)d_cf + (size_t)b0 * x->r * es_cf) : nullptr;
     static const bool no_fuse = getenv("BB_NO_FUSE_PREP") != nullptr;
-    const bool fuse_c = !no_fuse && need_content &&
-                        ((s3_c && gather_c) ||
-                         (scan_c && (gather_c || (x->dtype == F32 && q->q_dtype == F32 && x->d % 4 == 0 && rows_c &&
-                                                  ((uintptr_t)rows_c & 15) == 0))));
+    const bool fuse_c = !no_fuse && need_content && scan_c &&
+                        (gather_c || (x->dtype == F32 && q->q_dtype == F32 && x->d % 4 == 0 && rows_c &&
+                                      ((uintptr_t)rows_c & 15) == 0));
     const bool fuse_f = !no_fuse && scan_f && x->dtype == F32 && q->q_cf_dtype == F32 && x->r % 4 == 0 && rows_f &&
                         ((uintptr_t)rows_f & 15) == 0;
     if (need_content && !fuse_c) {
@@ -616,7 +615,6 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
           ga.X = (const char*)planes.p + (size_t)c0 * 3 * w * 2;
           ga.ldx = 3 * w;
           ga.ldq = 3 * w;
-          if (ga.q_ids) ga.q_items_base = planes.p;
           if ((rc = timed(x, K_GEMM, s, [&] { return launch_scan3(ga, s); }))) return rc;
         } else if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(x->dtype, ga, s); }))) {
           return rc;

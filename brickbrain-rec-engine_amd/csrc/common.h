@@ -30,7 +30,7 @@ constexpr int kSelectThreads = 256;
 constexpr int kSelectStageMax = 32768;  // score row staged in LDS when n_cols <= this
 constexpr int kMaxKInt = 512;      // per-side internal list length limit (k_side + 1)
 
-enum Dtype : int { F32 = 0, BF16 = 1, F64 = 2, SPLIT3 = 3 /* prep output: bf16 planes [xh|xm|xl] */ };
+enum Dtype : int { F32 = 0, BF16 = 1, F64 = 2, SPLIT3 = 3 /* prep output: bf16 planes as the scan3 q3f image */ };
 
 struct GemmArgs {
   const void* Q;      // [Mpad][ldq]   queries (normalised), dtype of the index
@@ -59,7 +59,17 @@ struct GemmArgs {
   int64_t q_src_ld;
   int32_t q_d;              // real query width (chunks past it read as 0)
   int32_t q_normalize;      // L2-normalise q_src rows
+  uint64_t* trace;          // probe builds only (scan3 ABL & 256): per-workgroup timestamps
 };
+
+// scan3 query image ("q3f"): the bf16 planes of 32-query wave blocks in the order the scan
+// loads them.  For query row q (wave block q >> 5, row r = q & 31 inside it), plane P and
+// 16-B chunk c (k-step u = c >> 1, half h = c & 1), the chunk sits at lane h·32 + r of the
+// 1-KiB line (block, P, u).  U = 16-wide k steps per row (Dpad / 16).
+__host__ __device__ inline size_t q3f_chunk_offset(int q, int c, int P, int U) {
+  const int lane = ((c & 1) << 5) | (q & 31);
+  return ((((size_t)(q >> 5) * 3 + P) * U + (c >> 1)) * 64 + lane) * 16;
+}
 
 struct SelectArgs {
   const float* S;           // scores [B][lds]
@@ -131,7 +141,7 @@ struct MaskArgs {
 hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s);
 bool gemm_uses_scan(int dtype, int Mpad, int Kpad);  // the query-resident scan kernel runs
 bool scan3_supported(int Mpad, int Kpad);            // split-bf16 scan for an f32 index
-hipError_t launch_scan3(const GemmArgs& a, hipStream_t s);  // X / q_items_base = planes
+hipError_t launch_scan3(const GemmArgs& a, hipStream_t s);  // X = item planes, Q = q3f image
 hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t* dst, hipStream_t s);
 int gemm_tile_m(int dtype);
 int gemm_tile_n(int dtype);

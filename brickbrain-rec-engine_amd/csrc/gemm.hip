@@ -96,7 +96,9 @@ static void launch_scan3_t(const GemmArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_scan3(const GemmArgs& a, hipStream_t s) {
-  if (!scan3_supported(a.Mpad, a.Kpad) || a.Ncols % 32 || (a.slab_start & 31)) return hipErrorInvalidValue;
+  // queries only as the prep kernel's q3f image: no fused gather / raw-row prologue here
+  if (!scan3_supported(a.Mpad, a.Kpad) || a.Ncols % 32 || (a.slab_start & 31) || a.q_ids || a.q_src)
+    return hipErrorInvalidValue;
   switch (a.Kpad * 2 / 16) {
     case 8: launch_scan3_t<8>(a, s); break;
     case 16: launch_scan3_t<16>(a, s); break;

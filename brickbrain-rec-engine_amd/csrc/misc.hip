@@ -153,15 +153,19 @@ __device__ __forceinline__ void split3_bits(float v, uint16_t& h, uint16_t& m, u
   l = (uint16_t)rne(r - __uint_as_float(mb << 16));
 }
 
-// store element i of output row `row` (index dtype, or SPLIT3 planes with row stride 3·Dpad)
+// store element i of output row `row`: index dtype, or SPLIT3 planes in the scan3 fragment
+// image (q3f_chunk_offset, scan3_kernel.h), so each query load of the scan is one 1-KiB
+// coalesced wave access
 __device__ __forceinline__ void store_q(const PrepArgs& a, int row, int i, float v) {
   if (a.out_dtype == SPLIT3) {
-    uint16_t* o = (uint16_t*)a.out + (size_t)row * 3 * a.Dpad + i;
+    const int U = a.Dpad >> 4;
+    uint16_t* o = (uint16_t*)((char*)a.out + q3f_chunk_offset(row, i >> 3, 0, U)) + (i & 7);
+    const size_t plane = (size_t)U * 64 * 8;  // bf16 elements between planes of one wave
     uint16_t h, m, l;
     split3_bits(v, h, m, l);
     o[0] = h;
-    o[a.Dpad] = m;
-    o[2 * a.Dpad] = l;
+    o[plane] = m;
+    o[2 * plane] = l;
   } else {
     store_elem(a.out, a.out_dtype, (size_t)row * a.Dpad + i, v);
   }

@@ -20,9 +20,9 @@
 // * Items are stored as planes per row, [xh | xm | xl], each KP 16-B chunks
 //   (row = 3·KP·16 bytes). They are staged 32 rows per tile by LDS-DMA into an
 //   XOR-swizzled double buffer. The swizzle keeps every chunk inside its plane.
-// * Queries are split in the prologue from f32 rows (raw rows normalised in-kernel, or
-//   prepared rows), or read as planes of stored items (q_ids). qh and qm are resident in
-//   AGPRs, ql in VGPRs.
+// * Queries come split by the prep kernel, as a "q3f" image in load order (common.h), so
+//   each of the 3·U query loads per lane is one coalesced 1-KiB wave access. They are
+//   issued behind the first tile's LDS-DMA. qh and qm are resident in AGPRs, ql in VGPRs.
 // * Epilogue and select contract are identical to scan2_kernel.h.
 #pragma once
 #include "scan2_kernel.h"
@@ -31,34 +31,24 @@ namespace bb {
 
 constexpr int kScan3MaxKP = 48;  // 2 tiles of 32 rows × 3 planes × 768 B = 144 KiB LDS
 
-// Query planes of this lane: chunk (2u + h) of each plane, u < KP/2, from rows of three
-// bf16 planes: the stored item rows of liked sets (q_ids, row stride ldx) or the prep
-// kernel's SPLIT3 output (Q, row stride ldq, both in bf16 elements).  Splitting happens
-// once per query in prep, not once per workgroup here (~3K VALU per wave otherwise).
+// Query planes of this lane from the prep kernel's q3f image (common.h): chunk (2u + h) of
+// each plane of query q, one coalesced 1-KiB wave load per (plane, u).  Rows past M_valid
+// are zero rows written by prep.
 template <int KP>
-__device__ __forceinline__ void scan3_load_queries(const GemmArgs& a, int q, int h, u32x4v (&qh)[KP / 2],
+__device__ __forceinline__ void scan3_load_queries(const GemmArgs& a, int q, int lane, u32x4v (&qh)[KP / 2],
                                                    u32x4v (&qm)[KP / 2], u32x4v (&ql)[KP / 2]) {
   constexpr int U = KP / 2;
-  const char* row;
-  bool ok = q < a.M_valid;
-  if (a.q_ids) {
-    const int64_t lid = ok ? a.q_ids[q] - a.q_id_offset : 0;
-    ok = ok && lid >= 0 && lid < a.q_n_items;
-    row = (const char*)a.q_items_base + (size_t)(ok ? lid : 0) * a.ldx * 2;
-  } else {
-    row = (const char*)a.Q + (size_t)(ok ? q : 0) * a.ldq * 2;
-  }
-  const u32x4v z = {0, 0, 0, 0};
+  const char* blk = (const char*)a.Q + (size_t)(q >> 5) * 3 * U * 1024 + lane * 16;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int c = 2 * u + h;
-    qh[u] = ok ? *(const u32x4v*)(row + c * 16) : z;
-    qm[u] = ok ? *(const u32x4v*)(row + (KP + c) * 16) : z;
-    ql[u] = ok ? *(const u32x4v*)(row + (2 * KP + c) * 16) : z;
+    qh[u] = *(const u32x4v*)(blk + u * 1024);
+    qm[u] = *(const u32x4v*)(blk + (U + u) * 1024);
+    ql[u] = *(const u32x4v*)(blk + (2 * U + u) * 1024);
   }
 }
 
-// KP: 16-B chunks per plane row (Dpad·2/16).  ABL: as scan2 (probe only).
+// KP: 16-B chunks per plane row (Dpad·2/16).  ABL: as scan2, plus 64 = no query loads and
+// 128 = no first-tile staging, 256 = timeline into a.trace (probe only).
 template <int KP, int ABL = 0>
 __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, int n_chunks, int tiles_total) {
   constexpr int U = KP / 2;                 // 16-wide k steps per tile
@@ -83,14 +73,15 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
   const int r = lane & 31, h = lane >> 5;
   const int q = group * kScanWaves * 32 + wave * 32 + r;
   if (tile_lo >= tile_hi) return;  // uniform per workgroup
-
-  u32x4v qh[U], qm[U], ql[U];
-  scan3_load_queries<KP>(a, q, h, qh, qm, ql);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    asm volatile("" : "+a"(qh[u]));
-    asm volatile("" : "+a"(qm[u]));
-  }
+  // probe-only timeline: s_memrealtime (100 MHz) per phase, s_memtime (core clock) span
+  auto stamp = [&](int slot) __attribute__((always_inline)) {
+    if constexpr (ABL & 256) {
+      if (tid == 0) a.trace[blockIdx.x * 32 + slot] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  uint64_t clk0 = 0;
+  if constexpr (ABL & 256) clk0 = __builtin_amdgcn_s_memtime();
+  stamp(0);
 
   // swizzle: chunk c of a row sits at c ^ (r & 15) (KP % 16 == 0) or c ^ (r & 7) (KP == 8);
   // both keep the chunk inside its plane (planes start at multiples of 8 chunks)
@@ -116,10 +107,31 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
   const uint32_t* erow = a.excl + (size_t)(q < a.M_valid ? q : a.M_valid - 1) * a.excl_ld;
   float* Srow = a.S + (size_t)q * a.lds;
 
+  // first tile's LDS-DMA ahead of the query loads: both streams are in flight together
+  if constexpr (!(ABL & 128)) {
 #pragma unroll
-  for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
+    for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
+  }
+  u32x4v qh[U], qm[U], ql[U];
+  if constexpr (ABL & 64) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) qh[u] = qm[u] = ql[u] = u32x4v{0, 0, 0, 0};
+  } else {
+    scan3_load_queries<KP>(a, q, lane, qh, qm, ql);
+  }
+  if constexpr (ABL & 256) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(1);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    asm volatile("" : "+a"(qh[u]));
+    asm volatile("" : "+a"(qm[u]));
+  }
+
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  stamp(2);
   asm volatile("s_nop 4");
 
   f32x16s accE = {}, accO = {};
@@ -241,18 +253,28 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
   tile_body(B0{}, EN{}, tile_lo, accE, accO);
   int tile = tile_lo + 1;
   for (;;) {
+    stamp(2 + tile - tile_lo);
     if (tile >= tile_hi) {
       last_epilogue(tile - 1, accE);
       break;
     }
     tile_body(B1{}, EY{}, tile, accO, accE);
     ++tile;
+    stamp(2 + tile - tile_lo);
     if (tile >= tile_hi) {
       last_epilogue(tile - 1, accO);
       break;
     }
     tile_body(B0{}, EY{}, tile, accE, accO);
     ++tile;
+  }
+  if constexpr (ABL & 256) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(29);
+    if (tid == 0) {
+      a.trace[blockIdx.x * 32 + 30] = __builtin_amdgcn_s_memtime() - clk0;
+      a.trace[blockIdx.x * 32 + 31] = (uint64_t)(tile_hi - tile_lo);
+    }
   }
 }
 

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 #include "../brickbrain-rec-engine_amd/csrc/scan3_kernel.h"
@@ -49,9 +50,10 @@ int main() {
       const uint16_t h = rne(v);
       const float r = v - bf(h);
       const uint16_t m = rne(r);
-      qplanes[(size_t)i * 3 * D + k] = h;
-      qplanes[(size_t)i * 3 * D + D + k] = m;
-      qplanes[(size_t)i * 3 * D + 2 * D + k] = rne(r - bf(m));
+      const size_t o = q3f_chunk_offset(i, k >> 3, 0, D / 16) / 2 + (k & 7), pl = (size_t)D / 16 * 512;
+      qplanes[o] = h;
+      qplanes[o + pl] = m;
+      qplanes[o + 2 * pl] = rne(r - bf(m));
     }
   std::vector<uint16_t> planes((size_t)N * 3 * D);
   for (int i = 0; i < N; ++i)
@@ -165,5 +167,65 @@ int main() {
   if (!timeit("no_staging", [&] { hipLaunchKernelGGL((scan3_kernel<48, 2>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32); })) return 1;
   if (!timeit("no_barrier", [&] { hipLaunchKernelGGL((scan3_kernel<48, 4>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32); })) return 1;
   if (!timeit("mfma_lds_only", [&] { hipLaunchKernelGGL((scan3_kernel<48, 7>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32); })) return 1;
+  // fixed cost vs per-tile slope: k tiles per workgroup (chunks * k <= N / 32 tiles exist)
+  auto run = [&](const char* base, int k, auto kern) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "%s_k%d", base, k);
+    return timeit(nm, [&] { hipLaunchKernelGGL(kern, dim3(2 * chunks), dim3(256), 0, 0, a, chunks, chunks * k); });
+  };
+  for (int k : {1, 6}) {
+    if (!run("full", k, scan3_kernel<48, 0>)) return 1;
+    if (!run("no_S_store", k, scan3_kernel<48, 8>)) return 1;
+    if (!run("no_max_store", k, scan3_kernel<48, 16>)) return 1;
+    if (!run("no_tile_maxima", k, scan3_kernel<48, 32>)) return 1;
+    if (!run("no_epilogue", k, scan3_kernel<48, 1>)) return 1;
+    if (!run("mfma_lds_only", k, scan3_kernel<48, 7>)) return 1;
+    if (!run("mfma_lds_noq", k, scan3_kernel<48, 7 | 64>)) return 1;
+    if (!run("mfma_lds_nofirst", k, scan3_kernel<48, 7 | 128>)) return 1;
+    if (!run("mfma_lds_noq_nofirst", k, scan3_kernel<48, 7 | 64 | 128>)) return 1;
+    if (!run("full_noq", k, scan3_kernel<48, 64>)) return 1;
+  }
+  // timelines (ABL 256): per workgroup, s_memrealtime at entry / queries loaded / first
+  // tile staged / after each tile / end, and the core-clock span
+  uint64_t* dtr;
+  (void)hipMalloc(&dtr, 2 * chunks * 32 * 8);
+  a.trace = dtr;
+  auto trace = [&](const char* name, int tiles, auto kern) {
+    for (int w = 0; w < 5; ++w) hipLaunchKernelGGL(kern, dim3(2 * chunks), dim3(256), 0, 0, a, chunks, tiles);
+    (void)hipMemset(dtr, 0, 2 * chunks * 32 * 8);
+    hipLaunchKernelGGL(kern, dim3(2 * chunks), dim3(256), 0, 0, a, chunks, tiles);
+    if (hipDeviceSynchronize() != hipSuccess) return false;
+    std::vector<uint64_t> tr(2 * chunks * 32);
+    (void)hipMemcpy(tr.data(), dtr, tr.size() * 8, hipMemcpyDeviceToHost);
+    uint64_t t0 = ~0ull, tend = 0;
+    double qload = 0, first = 0, span = 0, ghz = 0, tiles_sum[8] = {0}, start_max = 0;
+    int nt_cnt[8] = {0};
+    for (int b = 0; b < 2 * chunks; ++b) t0 = std::min(t0, tr[b * 32]);
+    for (int b = 0; b < 2 * chunks; ++b) {
+      const uint64_t* r = &tr[b * 32];
+      const int nt = (int)r[31];
+      qload += (r[1] - r[0]) * 10.0;
+      first += (r[2] - r[1]) * 10.0;
+      span += (r[29] - r[0]) * 10.0;
+      ghz += r[30] / ((r[29] - r[0]) * 10.0);
+      start_max = std::max(start_max, (r[0] - t0) * 10.0);
+      tend = std::max(tend, r[29]);
+      for (int j = 0; j < nt && j < 8; ++j) { tiles_sum[j] += (r[3 + j] - r[2 + j]) * 10.0; nt_cnt[j]++; }
+    }
+    const double n = 2 * chunks;
+    printf("{\"trace\":\"%s\",\"ns_qload\":%.0f,\"ns_first_tile\":%.0f,\"ns_wg_span\":%.0f,\"ns_grid\":%.0f,"
+           "\"ns_last_start\":%.0f,\"memtime_per_ns\":%.3f,\"ns_tiles\":[",
+           name, qload / n, first / n, span / n, (tend - t0) * 10.0, start_max, ghz / n);
+    for (int j = 0; j < 8; ++j) printf("%s%.0f", j ? "," : "", nt_cnt[j] ? tiles_sum[j] / nt_cnt[j] : 0.0);
+    printf("]}\n");
+    return true;
+  };
+  if (!trace("full", N / 32, scan3_kernel<48, 256>)) return 1;
+  if (!trace("no_epilogue", N / 32, scan3_kernel<48, 256 | 1>)) return 1;
+  if (!trace("mfma_lds_only", N / 32, scan3_kernel<48, 256 | 7>)) return 1;
+  if (!trace("full_k1", chunks, scan3_kernel<48, 256>)) return 1;
+  a.trace = nullptr;
+  // empty grid (tiles 0: every workgroup returns at once) = launch + gap
+  if (!timeit("empty_grid", [&] { hipLaunchKernelGGL((scan3_kernel<48, 0>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, 0); })) return 1;
   return 0;
 }
