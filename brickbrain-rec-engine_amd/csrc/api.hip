@@ -634,6 +634,7 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
         sa.excl = cf_side && d_excl ? (const uint32_t*)d_excl + (size_t)b0 * nw : nullptr;
         sa.excl_ld = nw;
         sa.K = K_int;
+        sa.s_blocked = (cf_side ? s3_f : s3_c) ? 1 : 0;
         sa.carry_in = sl ? keys + ((size_t)(pp ^ 1) * sides + side) * side_keys : nullptr;
         sa.keys_out = keys + ((size_t)pp * sides + side) * side_keys;
         sa.max_inout = side_drop ? maxk : nullptr;

@@ -71,6 +71,24 @@ __host__ __device__ inline size_t q3f_chunk_offset(int q, int c, int P, int U) {
   return ((((size_t)(q >> 5) * 3 + P) * U + (c >> 1)) * 64 + lane) * 16;
 }
 
+// scan3 item image ("t3"): the three bf16 planes of each 32-row tile in LDS order, one
+// contiguous block of 32·3·Dpad·2 bytes per tile.  Plane P, 16-B chunk c (8 elements), row r
+// of tile t sits at t·TILE_B + ((P·KP + c)·32 + r)·16 with KP = Dpad / 8.  One wave's 1-KiB
+// LDS-DMA piece and one wave's ds_read_b128 fragment (chunks 2u, 2u+1 of 32 rows) are both
+// contiguous.  Returns the byte offset of the chunk.
+__host__ __device__ inline size_t t3_chunk_offset(int64_t row, int c, int P, int Dpad) {
+  const int KP = Dpad >> 3;
+  return (size_t)(row >> 5) * 32 * 3 * Dpad * 2 + ((size_t)(P * KP + c) * 32 + (row & 31)) * 16;
+}
+
+// scan3 score image ("blocked S"): each (32-query block, tile) accumulator stored as the MFMA
+// leaves it, 4 KiB contiguous, so the scan's score stores are full 1-KiB wave writes.  Items
+// 4g..4g+3 (g = item >> 2 within the tile) of query q are the float4 at the returned float
+// offset; ldt = tiles per query row.
+__host__ __device__ inline size_t sblk_quad(int q, int t, int g, int64_t ldt) {
+  return (((size_t)(q >> 5) * ldt + t) * 4 + (g >> 1)) * 256 + (((g & 1) << 5) | (q & 31)) * 4;
+}
+
 struct SelectArgs {
   const float* S;           // scores [B][lds]
   int64_t lds;
@@ -94,6 +112,7 @@ struct SelectArgs {
   int64_t* out_ids;         // [B][k_final]
   int32_t* out_counts;      // [B] or null
   int32_t k_final;
+  int32_t s_blocked;        // S is the scan3 blocked image (sblk_quad), else row-major [B][lds]
 };
 
 struct FinalizeArgs {

@@ -73,30 +73,51 @@ hipError_t launch_convert_rows(const void* src, int src_dtype, int64_t n, int d,
   return hipGetLastError();
 }
 
-// f32 rows -> three bf16 planes per row ([xh | xm | xl], x = xh + xm + xl exactly) for the
-// split-precision scan (scan3_kernel.h).  One thread per element.
-__global__ __launch_bounds__(256) void split_planes_kernel(const float* src, int64_t n, int64_t ld, uint16_t* dst) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n * ld) return;
-  const int64_t row = i / ld, col = i - row * ld;
-  const float v = src[i];
+__device__ __forceinline__ void split3_bits(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
   auto rne = [](float f) -> uint32_t {
     uint32_t u = __float_as_uint(f);
     u += 0x7FFFu + ((u >> 16) & 1u);
     return u >> 16;
   };
-  const uint32_t h = rne(v);
-  const float r = v - __uint_as_float(h << 16);
-  const uint32_t m = rne(r);
-  const uint32_t l = rne(r - __uint_as_float(m << 16));
-  uint16_t* o = dst + row * 3 * ld + col;
-  o[0] = (uint16_t)h;
-  o[ld] = (uint16_t)m;
-  o[2 * ld] = (uint16_t)l;
+  const uint32_t hb = rne(v);
+  const float r = v - __uint_as_float(hb << 16);
+  const uint32_t mb = rne(r);
+  h = (uint16_t)hb;
+  m = (uint16_t)mb;
+  l = (uint16_t)rne(r - __uint_as_float(mb << 16));
+}
+
+// f32 rows -> three bf16 planes (x = xh + xm + xl exactly) in the scan3 tile image
+// (t3_chunk_offset, common.h).  One thread per 8-element chunk of a row: 32 B read, three
+// 16-B plane chunks written.
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* src, int64_t n, int64_t ld, uint16_t* dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t cpr = ld >> 3;
+  if (i >= n * cpr) return;
+  const int64_t row = i / cpr;
+  const int c = (int)(i - row * cpr);
+  const float4 v0 = *(const float4*)(src + row * ld + 8 * c);
+  const float4 v1 = *(const float4*)(src + row * ld + 8 * c + 4);
+  const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint16_t h0, m0, l0, h1, m1, l1;
+    split3_bits(v[2 * k], h0, m0, l0);
+    split3_bits(v[2 * k + 1], h1, m1, l1);
+    hw[k] = h0 | ((uint32_t)h1 << 16);
+    mw[k] = m0 | ((uint32_t)m1 << 16);
+    lw[k] = l0 | ((uint32_t)l1 << 16);
+  }
+  char* o = (char*)dst;
+  *(uint4*)(o + t3_chunk_offset(row, c, 0, (int)ld)) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+  *(uint4*)(o + t3_chunk_offset(row, c, 1, (int)ld)) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+  *(uint4*)(o + t3_chunk_offset(row, c, 2, (int)ld)) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
 }
 
 hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t* dst, hipStream_t s) {
-  const int64_t total = n * ld;
+  if (n % 32 || ld % 8) return hipErrorInvalidValue;  // whole tiles, whole chunks
+  const int64_t total = n * (ld >> 3);
   if (total <= 0) return hipSuccess;
   hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, src, n, ld, dst);
   return hipGetLastError();
@@ -139,19 +160,6 @@ __device__ __forceinline__ void load_chunk(const void* p, int dt, size_t sb, int
 constexpr int kPrepC = 8;  // rows up to 512 wide stay in registers (one load round)
 
 // f32 -> three bf16 planes (x = xh + xm + xl exactly) for the split-precision scan
-__device__ __forceinline__ void split3_bits(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
-  auto rne = [](float f) -> uint32_t {
-    uint32_t u = __float_as_uint(f);
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return u >> 16;
-  };
-  const uint32_t hb = rne(v);
-  const float r = v - __uint_as_float(hb << 16);
-  const uint32_t mb = rne(r);
-  h = (uint16_t)hb;
-  m = (uint16_t)mb;
-  l = (uint16_t)rne(r - __uint_as_float(mb << 16));
-}
 
 // store element i of output row `row`: index dtype, or SPLIT3 planes in the scan3 fragment
 // image (q3f_chunk_offset, scan3_kernel.h), so each query load of the scan is one 1-KiB

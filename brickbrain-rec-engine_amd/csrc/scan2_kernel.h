@@ -102,11 +102,18 @@ __device__ __forceinline__ void scan2_load_queries(const GemmArgs& a, int q, int
 __device__ __forceinline__ void tile_maxima(const f32x16s& p, int tile0, int n_valid, uint32_t pw, uint32_t ok, int h,
                                             uint32_t& te, uint32_t& tp) {
   if (__all(tile0 + 32 <= n_valid && pw == 0xFFFFFFFFu && ok == 0xFFFFFFFFu)) {
-    const float m0 = fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3]));
-    const float m1 = fmaxf(fmaxf(p[4], p[5]), fmaxf(p[6], p[7]));
-    const float m2 = fmaxf(fmaxf(p[8], p[9]), fmaxf(p[10], p[11]));
-    const float m3 = fmaxf(fmaxf(p[12], p[13]), fmaxf(p[14], p[15]));
-    te = tp = ord_of(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)) + 0.0f);
+    // v_max3_f32 directly: fmaxf on opaque (inline-asm MFMA) results would canonicalise
+    // every input first, doubling the count.  Scores are finite, so NaN rules do not apply.
+    auto max3 = [](float x, float y, float z) {
+      float m;
+      asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(x), "v"(y), "v"(z));
+      return m;
+    };
+    const float m0 = max3(p[0], p[1], p[2]), m1 = max3(p[3], p[4], p[5]), m2 = max3(p[6], p[7], p[8]);
+    const float m3 = max3(p[9], p[10], p[11]), m4 = max3(p[12], p[13], p[14]);
+    const float m = max3(max3(m0, m1, m2), max3(m3, m4, p[15]), p[15]);
+    const uint32_t u = __builtin_bit_cast(uint32_t, m + 0.0f);
+    te = tp = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);  // ord_of
     return;
   }
   uint32_t e = 0, t = 0;

@@ -17,13 +17,15 @@
 // epilogue overlaps.
 //
 // Layout:
-// * Items are stored as planes per row, [xh | xm | xl], each KP 16-B chunks
-//   (row = 3·KP·16 bytes). They are staged 32 rows per tile by LDS-DMA into an
-//   XOR-swizzled double buffer. The swizzle keeps every chunk inside its plane.
+// * Items are stored as the t3 tile image (common.h): per 32-row tile, plane-major 16-B
+//   chunks with the 32 rows of a chunk adjacent — the LDS order. Tiles are staged by
+//   LDS-DMA into a double buffer with contiguous 1-KiB pieces; fragment reads are
+//   contiguous 1-KiB wave reads (conflict-free, no swizzle).
 // * Queries come split by the prep kernel, as a "q3f" image in load order (common.h), so
 //   each of the 3·U query loads per lane is one coalesced 1-KiB wave access. They are
 //   issued behind the first tile's LDS-DMA. qh and qm are resident in AGPRs, ql in VGPRs.
-// * Epilogue and select contract are identical to scan2_kernel.h.
+// * Epilogue: per-tile maxima as scan2_kernel.h; scores go out as the blocked image
+//   (sblk_quad, common.h) — each wave stores its accumulator as-is, 4 full 1-KiB writes.
 #pragma once
 #include "scan2_kernel.h"
 
@@ -31,20 +33,14 @@ namespace bb {
 
 constexpr int kScan3MaxKP = 48;  // 2 tiles of 32 rows × 3 planes × 768 B = 144 KiB LDS
 
-// Query planes of this lane from the prep kernel's q3f image (common.h): chunk (2u + h) of
-// each plane of query q, one coalesced 1-KiB wave load per (plane, u).  Rows past M_valid
-// are zero rows written by prep.
-template <int KP>
-__device__ __forceinline__ void scan3_load_queries(const GemmArgs& a, int q, int lane, u32x4v (&qh)[KP / 2],
-                                                   u32x4v (&qm)[KP / 2], u32x4v (&ql)[KP / 2]) {
-  constexpr int U = KP / 2;
-  const char* blk = (const char*)a.Q + (size_t)(q >> 5) * 3 * U * 1024 + lane * 16;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    qh[u] = *(const u32x4v*)(blk + u * 1024);
-    qm[u] = *(const u32x4v*)(blk + (U + u) * 1024);
-    ql[u] = *(const u32x4v*)(blk + (2 * U + u) * 1024);
-  }
+// Query planes of this lane for k-step u from the prep kernel's q3f image (common.h):
+// chunk (2u + h) of each plane of query q, three coalesced 1-KiB wave loads.  Rows past
+// M_valid are zero rows written by prep.
+template <int U>
+__device__ __forceinline__ void scan3_load_query_step(const char* blk, int u, u32x4v& qh, u32x4v& qm, u32x4v& ql) {
+  qh = *(const u32x4v*)(blk + u * 1024);
+  qm = *(const u32x4v*)(blk + (U + u) * 1024);
+  ql = *(const u32x4v*)(blk + (2 * U + u) * 1024);
 }
 
 // KP: 16-B chunks per plane row (Dpad·2/16).  ABL: as scan2, plus 64 = no query loads and
@@ -55,7 +51,6 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
   constexpr int ROWB = 3 * KP * 16;         // bytes of one item row (three planes)
   constexpr int TILE_B = 32 * ROWB;
   constexpr int PIECES = TILE_B / (1024 * kScanWaves);
-  constexpr int G = 8;                      // KP % 16 == 0 or KP == 8: swizzle period 8 u-steps
   static_assert(KP % 8 == 0 && KP <= kScan3MaxKP, "unsupported plane width");
   static_assert(TILE_B % (1024 * kScanWaves) == 0, "tile must split into whole 1 KiB pieces per wave");
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE_B];
@@ -83,53 +78,59 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
   if constexpr (ABL & 256) clk0 = __builtin_amdgcn_s_memtime();
   stamp(0);
 
-  // swizzle: chunk c of a row sits at c ^ (r & 15) (KP % 16 == 0) or c ^ (r & 7) (KP == 8);
-  // both keep the chunk inside its plane (planes start at multiples of 8 chunks)
-  constexpr int SWM = (KP % 16 == 0) ? 15 : 7;
-  const int swz = r & SWM;
-  int rd[G];
-#pragma unroll
-  for (int m = 0; m < G; ++m) rd[m] = r * ROWB + (((2 * m + h) ^ swz) << 4);
-
+  // Items come as the t3 tile image (common.h): a tile is one contiguous block in LDS order,
+  // so a wave's 1-KiB LDS-DMA piece is a contiguous 1 KiB of HBM (uniform SGPR address plus
+  // a constant lane offset, no per-tile vector arithmetic), and the fragment of plane P at
+  // u-step u (chunks 2u, 2u+1 of all 32 rows) is the contiguous 1 KiB at (P·KP + 2u)·512.
   const char* Xg = (const char*)a.X;
-  const size_t ldxb = (size_t)a.ldx * 2;  // = ROWB (planes of one row are contiguous)
   const uint32_t lds_base = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+  const int lane16 = lane * 16;
+  uint32_t lb[2][2];  // fragment read bases: buffer b, offsets below / from 32 KiB
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    lb[b][0] = lds_base + b * TILE_B + lane16;
+    lb[b][1] = lb[b][0] + 32768;
+    asm volatile("" : "+v"(lb[b][0]), "+v"(lb[b][1]));
+  }
   auto stage_piece = [&](int tile, int buf, int p) __attribute__((always_inline)) {
-    const int mine = (wave * PIECES + p) * 1024 + lane * 16;
-    const int row = mine / ROWB;
-    const int ch = ((mine % ROWB) >> 4) ^ (row & SWM);
-    const char* src = Xg + ((size_t)tile * 32 + row) * ldxb + ch * 16;
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + buf * TILE_B + (wave * PIECES + p) * 1024);
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory");
+    const int pc = wave * PIECES + p;
+    const char* src = Xg + (size_t)tile * TILE_B + pc * 1024;
+    const uint32_t dst = lds_base + buf * TILE_B + pc * 1024;
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(dst), "v"(lane16), "s"(src)
+                 : "memory");
   };
 
   const size_t w0 = (size_t)(a.slab_start >> 5);
   const uint32_t* erow = a.excl + (size_t)(q < a.M_valid ? q : a.M_valid - 1) * a.excl_ld;
-  float* Srow = a.S + (size_t)q * a.lds;
+  // blocked score image (sblk_quad): this wave's 4-KiB block per tile, lane-linear
+  float* Sblk = a.S + (size_t)(q >> 5) * a.ldt * 1024 + lane * 4;
 
   // first tile's LDS-DMA ahead of the query loads: both streams are in flight together
   if constexpr (!(ABL & 128)) {
 #pragma unroll
     for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
   }
+  // Query stream: k-steps [0, QD) load here, behind the first tile's pieces; steps
+  // [QD, U) load inside the first tile, QD steps ahead of their MFMAs, so the ~288 KiB of
+  // queries per workgroup stream in under the first tile's MFMAs.  The compiler waits for
+  // each query register at its first use (pinned to AGPRs there).
+  constexpr int QD = U / 2;
+  const char* qblk = (const char*)a.Q + (size_t)(q >> 5) * 3 * U * 1024 + lane16;
   u32x4v qh[U], qm[U], ql[U];
-  if constexpr (ABL & 64) {
+  auto load_q = [&](int u) __attribute__((always_inline)) {
+    if constexpr (ABL & 64) {
+      qh[u] = qm[u] = ql[u] = u32x4v{0, 0, 0, 0};
+    } else {
+      scan3_load_query_step<U>(qblk, u, qh[u], qm[u], ql[u]);
+      asm volatile("" ::: "memory");  // keep the step order: the waits count on it
+    }
+  };
 #pragma unroll
-    for (int u = 0; u < U; ++u) qh[u] = qm[u] = ql[u] = u32x4v{0, 0, 0, 0};
-  } else {
-    scan3_load_queries<KP>(a, q, lane, qh, qm, ql);
-  }
-  if constexpr (ABL & 256) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp(1);
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    asm volatile("" : "+a"(qh[u]));
-    asm volatile("" : "+a"(qm[u]));
-  }
-
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int u = 0; u < QD; ++u) load_q(u);
+  stamp(1);  // prologue loads issued
+  // loads retire in order: once at most the 3·QD query loads are outstanding, the older
+  // pieces of the first tile have landed
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * QD) : "memory");
   __syncthreads();
   stamp(2);
   asm volatile("s_nop 4");
@@ -142,13 +143,17 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
   auto tile_body = [&](auto BUF, auto EPI, int tile, f32x16s& c, const f32x16s& p) __attribute__((always_inline)) {
     constexpr int buf = decltype(BUF)::value;
     constexpr bool epi = decltype(EPI)::value && !(ABL & 1);
+    constexpr bool first = !decltype(EPI)::value;  // the first tile (streams the queries)
     const int ptile = tile - 1;
     const int stile = tile + 1 < tile_hi ? tile + 1 : tile;
     uint32_t te = 0, tp = 0;
     const int ptile0 = ptile * 32;
     // fragment of plane P at u-step u: ds_read two steps ahead
+    // (two base registers per buffer keep every ds_read offset inside its 16-bit field)
     auto frag = [&](int P, int u) __attribute__((always_inline)) {
-      return *(const u32x4v*)(smem + buf * TILE_B + rd[u % G] + (u / G) * G * 32 + P * KP * 16);
+      const int off = (P * KP + 2 * u) * 512;
+      const uint32_t base = off < 32768 ? lb[buf][0] : lb[buf][1];
+      return *(const __attribute__((address_space(3))) u32x4v*)(size_t)(base + (off < 32768 ? off : off - 32768));
     };
     // 4-slot ring, prefetch distance 2.  Inline-asm MFMAs are opaque to the compiler's
     // hazard tracking, so a fragment's registers are kept live (empty asm use) until the
@@ -171,6 +176,10 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
         fl[(u + 2) % 4] = frag(2, u + 2);
       }
       const u32x4v xh = fh[u % 4], xm = fm[u % 4], xl = fl[u % 4];
+      if constexpr (first) {
+        if constexpr (u + QD < U) load_q(u + QD);
+        asm volatile("" : "+a"(qh[u]), "+a"(qm[u]));
+      }
       // one accumulation chain, largest term first
       if constexpr (u == 0)
         asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(xh), "a"(qh[u]));
@@ -189,7 +198,9 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
       // latency has most of the tile to land), then the previous tile's epilogue
       static_for<kEpiSlices>([&](auto SS) {
         constexpr int s = decltype(SS)::value;
-        constexpr int s_stage = (s - 8) / 2;
+        // staging: two pieces per u-step, from step 0; in the first tile only after its
+        // last query loads, so no query wait ever covers a freshly issued piece
+        constexpr int s_stage = (first ? QD : 0) + (s - 8) / 2;
         constexpr int s_epi = U / 2 + s;
         constexpr int su0 = s >= 8 ? s_stage : s_epi;
         constexpr int su = su0 < U ? su0 : U - 1;
@@ -205,7 +216,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
           } else if constexpr (s < 6) {
             if constexpr (epi && !(ABL & 8)) {
               constexpr int j = s - 2;
-              *(float4*)(Srow + ptile0 + 8 * j + 4 * h) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+              *(float4*)(Sblk + (size_t)ptile * 1024 + j * 256) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
             }
           } else if constexpr (s == 6) {
             if constexpr (epi && !(ABL & 16)) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
@@ -242,7 +253,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
     tp = tp2 > tp ? tp2 : tp;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      *(float4*)(Srow + tile * 32 + 8 * j + 4 * h) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+      *(float4*)(Sblk + (size_t)tile * 1024 + j * 256) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
     (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
   };
 

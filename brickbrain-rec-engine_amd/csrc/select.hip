@@ -302,6 +302,13 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   const int n = a.n_cols, K = a.K;
   const int ntiles = (n + 31) >> 5;
   const float* Srow = a.S + (size_t)row * a.lds;
+  // four scores of items 4g..4g+3 of tile t (row-major S or the scan3 blocked image)
+  auto s_quad = [&](int t, int g) -> float4 {
+    return a.s_blocked ? *(const float4*)(a.S + sblk_quad(row, t, g, a.ldt)) : *(const float4*)(Srow + t * 32 + 4 * g);
+  };
+  auto s_at = [&](int j) -> float {
+    return a.s_blocked ? a.S[sblk_quad(row, j >> 5, (j >> 2) & 7, a.ldt) + (j & 3)] : Srow[j];
+  };
   const uint32_t* trow = a.tmax + (size_t)row * a.ldt;
   const uint32_t* prow = a.max_inout ? a.pmax + (size_t)row * a.ldt : nullptr;
   const uint32_t* excl = a.excl ? a.excl + (size_t)row * a.excl_ld : nullptr;
@@ -376,7 +383,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     r0_tile = (int)(0xFFFFFFFFu - (uint32_t)b);
     if (P0 && lane < 32) {
       const int j = r0_tile * 32 + lane;
-      r0_val = j < n ? Srow[j] : 0.f;
+      r0_val = j < n ? s_at(j) : 0.f;
       r0_word = a.present ? a.present[w0 + r0_tile] : ~0u;
     }
   }
@@ -448,7 +455,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   auto gather_tile = [&](int t) {
     float4 v[8];
 #pragma unroll
-    for (int c4 = 0; c4 < 8; ++c4) v[c4] = *(const float4*)(Srow + t * 32 + 4 * c4);
+    for (int c4 = 0; c4 < 8; ++c4) v[c4] = s_quad(t, c4);
     const uint32_t ok = elig(t);
 #pragma unroll
     for (int c4 = 0; c4 < 8; ++c4) {
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     __syncthreads();
     auto ord_at = [&](int j) -> uint32_t {
       const uint32_t ok = elig(j >> 5);
-      return ((ok >> (j & 31)) & 1u) ? ord_of(Srow[j]) : 0u;
+      return ((ok >> (j & 31)) & 1u) ? ord_of(s_at(j)) : 0u;
     };
     cnt = radix_select(ord_at, n, a.gid0, carry, K, cand, hist, misc, scan_sh);
   }

@@ -63,9 +63,9 @@ int main() {
       const float r = v - bf(h);
       const uint16_t m = rne(r);
       const uint16_t l = rne(r - bf(m));
-      planes[(size_t)i * 3 * D + k] = h;
-      planes[(size_t)i * 3 * D + D + k] = m;
-      planes[(size_t)i * 3 * D + 2 * D + k] = l;
+      planes[t3_chunk_offset(i, k >> 3, 0, D) / 2 + (k & 7)] = h;
+      planes[t3_chunk_offset(i, k >> 3, 1, D) / 2 + (k & 7)] = m;
+      planes[t3_chunk_offset(i, k >> 3, 2, D) / 2 + (k & 7)] = l;
     }
   float *dq, *dS;
   uint16_t* dx;
@@ -99,13 +99,14 @@ int main() {
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) { printf("{\"variant\":%d,\"error\":\"%s\"}\n", variant, hipGetErrorString(e)); return 1; }
     (void)hipMemcpy(S.data(), dS, S.size() * 4, hipMemcpyDeviceToHost);
+    auto SV = [&](int i, int j) { return S[sblk_quad(i, j >> 5, (j >> 2) & 7, N / 32) + (j & 3)]; };
     (void)hipMemcpy(T.data(), tm, T.size() * 4, hipMemcpyDeviceToHost);
     double maxerr = 0;
     for (int i = 0; i < M; i += 7)
       for (int j = 0; j < N; j += 13) {
         double ref = 0;
         for (int k = 0; k < D; ++k) ref += (double)q[(size_t)i * D + k] * x[(size_t)j * D + k];
-        maxerr = std::fmax(maxerr, std::fabs(ref - S[(size_t)i * N + j]));
+        maxerr = std::fmax(maxerr, std::fabs(ref - SV(i, j)));
       }
     {
       // locate wrong scores: by tile position inside its workgroup chunk, and by query row
@@ -118,7 +119,7 @@ int main() {
             const int col = t * 32 + j;
             double ref = 0;
             for (int k = 0; k < D; ++k) ref += (double)q[(size_t)i * D + k] * x[(size_t)col * D + k];
-            if (std::fabs(ref - S[(size_t)i * N + col]) > 1e-5) ++b;
+            if (std::fabs(ref - SV(i, col)) > 1e-5) ++b;
           }
           if (!b) continue;
           nbad += b;
@@ -136,7 +137,7 @@ int main() {
     for (int i = 0; i < M; ++i)
       for (int t = 0; t < N / 32; ++t) {
         float mx = -1e30f;
-        for (int j = 0; j < 32; ++j) mx = std::fmax(mx, S[(size_t)i * N + t * 32 + j]);
+        for (int j = 0; j < 32; ++j) mx = std::fmax(mx, SV(i, t * 32 + j));
         const uint32_t want = ord_of(mx + 0.0f), got = T[(size_t)i * (N / 32) + t];
         if (got != want) { ++bad; if (got < want) ++lower; if (got == 0) ++zero; }
       }
@@ -223,6 +224,11 @@ int main() {
   if (!trace("full", N / 32, scan3_kernel<48, 256>)) return 1;
   if (!trace("no_epilogue", N / 32, scan3_kernel<48, 256 | 1>)) return 1;
   if (!trace("mfma_lds_only", N / 32, scan3_kernel<48, 256 | 7>)) return 1;
+  if (!trace("no_staging", N / 32, scan3_kernel<48, 256 | 2>)) return 1;
+  if (!trace("no_S_store", N / 32, scan3_kernel<48, 256 | 8>)) return 1;
+  if (!trace("no_max_store", N / 32, scan3_kernel<48, 256 | 16>)) return 1;
+  if (!trace("no_tile_maxima", N / 32, scan3_kernel<48, 256 | 32>)) return 1;
+  if (!trace("no_stage_no_epi", N / 32, scan3_kernel<48, 256 | 3>)) return 1;
   if (!trace("full_k1", chunks, scan3_kernel<48, 256>)) return 1;
   a.trace = nullptr;
   // empty grid (tiles 0: every workgroup returns at once) = launch + gap
