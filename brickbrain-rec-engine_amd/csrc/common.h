@@ -113,6 +113,7 @@ struct SelectArgs {
   int32_t* out_counts;      // [B] or null
   int32_t k_final;
   int32_t s_blocked;        // S is the scan3 blocked image (sblk_quad), else row-major [B][lds]
+  uint64_t* trace;          // probe builds only: per-workgroup phase timestamps, or null
 };
 
 struct FinalizeArgs {

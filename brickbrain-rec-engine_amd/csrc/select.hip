@@ -324,8 +324,12 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     return *pp & *mp & ~*ep;
   };
 
+  // probe-only phase timeline (s_memrealtime, 100 MHz), thread 0
+  auto stamp = [&](int slot) {
+    if (a.trace && tid == 0) a.trace[row * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   if (tid == 0) {
-    misc[6] = 0;  // T0 (atomicMax)
     misc[7] = 0;  // candidate count
     misc[8] = 0;  // qualifying-tile count
     *(uint64_t*)(misc + 10) = 0ull;  // rank-0 key of this query
@@ -369,9 +373,10 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   }
   if constexpr (ABL == 1) { if (tm == 0x12345u) a.keys_out[row] = tm; return; }
   __syncthreads();  // B1
+  stamp(1);
 
   // ---- rank 0 (similar / hybrid content side): wave 0 reads the winning tile now and
-  // resolves it after B2, so its latency hides behind the bound computation ----
+  // resolves it after the bound, so its latency hides behind it ----
   uint32_t P0 = 0, r0_word = 0;
   int r0_tile = 0;
   float r0_val = 0.f;
@@ -388,23 +393,45 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     }
   }
 
-  // ---- bound: T0 = K-th largest per-thread max of the tile maxima ----
-  if (tm) {  // rank of my maximum among the 256 (16-B LDS reads, all independent)
-    uint32_t ge = 0;
-#pragma unroll 8
-    for (int t = 0; t < kSelectThreads; t += 4) {
-      const uint4 v = *(const uint4*)(tmx + t);
-      ge += (v.x >= tm) + (v.y >= tm) + (v.z >= tm) + (v.w >= tm);
+  // ---- bound: T0 = K-th largest per-thread max of the tile maxima (at least K eligible
+  // items are >= T0, so every top-K member is).  Every wave finds it on its own, no
+  // barrier: the 256 maxima as 4 per lane, then the largest C with #(maxima >= C) >= K,
+  // decided bit by bit below the common prefix of the extremes (ballot counts, scalar
+  // loop).  Fewer than K non-zero maxima: T0 = 0, i.e. every eligible item. ----
+  uint32_t T0 = 0;
+  {
+    const uint4 x = *(const uint4*)(tmx + 4 * lane);
+    auto cnt_ge = [&](uint32_t c) -> uint32_t {
+      return (uint32_t)(__popcll(__ballot(x.x >= c)) + __popcll(__ballot(x.y >= c)) + __popcll(__ballot(x.z >= c)) +
+                        __popcll(__ballot(x.w >= c)));
+    };
+    if (cnt_ge(1u) >= (uint32_t)K) {
+      uint32_t hi = max(max(x.x, x.y), max(x.z, x.w));
+      uint32_t lo = min(min(x.x ? x.x : ~0u, x.y ? x.y : ~0u), min(x.z ? x.z : ~0u, x.w ? x.w : ~0u));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+      }
+      hi = __builtin_amdgcn_readfirstlane(hi);
+      lo = __builtin_amdgcn_readfirstlane(lo);
+      const uint32_t d = hi ^ lo;
+      // bits above the highest differing one are shared by every non-zero maximum
+      const int top = d ? 31 - __builtin_clz(d) : -1;
+      uint32_t P = top < 0 ? hi : top >= 31 ? 0u : hi & ~((2u << top) - 1u);
+      for (int b = top; b >= 0; --b) {
+        const uint32_t c = P | (1u << b);
+        if (cnt_ge(c) >= (uint32_t)K) P = c;
+      }
+      T0 = P;
     }
-    if (ge >= (uint32_t)K) atomicMax(&misc[6], tm);
   }
-  __syncthreads();  // B2
-  uint32_t T0 = misc[6];
   if (carry) {
     const uint32_t ck = ordk_of(carry[K - 1]);  // K carried keys are >= ck
     T0 = ck > T0 ? ck : T0;
   }
   if (T0 == 0) T0 = 1;  // fewer than K threads see eligible items: take every eligible one
+  stamp(2);
   if constexpr (ABL == 2) { if (T0 == 0x12345u) a.keys_out[row] = T0; return; }
 
   if (prow && wave == 0) {
@@ -426,13 +453,30 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     }
   }
 
-  // ---- qualifying tiles -> compact list; carried keys -> candidates ----
+  // ---- qualifying tiles -> compact list (one LDS atomic per wave); carried keys ->
+  // candidates ----
+  {
+    uint64_t qm[kB];
+    uint32_t tot = 0;
 #pragma unroll
-  for (int b = 0; b < kB; ++b) {
-    const int t = tid + b * kSelectThreads;
-    if (t < ntiles && v0[b] >= T0) {
-      const uint32_t p = atomicAdd(&misc[8], 1u);
-      if (p < (uint32_t)kTileCap) tlist[p] = (uint32_t)t;
+    for (int b = 0; b < kB; ++b) {
+      const int t = tid + b * kSelectThreads;
+      qm[b] = __ballot(t < ntiles && v0[b] >= T0);
+      tot += (uint32_t)__popcll(qm[b]);
+    }
+    if (tot) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&misc[8], tot);
+      base = (uint32_t)__shfl((int)base, 0);
+#pragma unroll
+      for (int b = 0; b < kB; ++b) {
+        const uint32_t lo32 = (uint32_t)qm[b], hi32 = (uint32_t)(qm[b] >> 32);
+        if ((qm[b] >> lane) & 1ull) {
+          const uint32_t p = base + __builtin_amdgcn_mbcnt_hi(hi32, __builtin_amdgcn_mbcnt_lo(lo32, 0u));
+          if (p < (uint32_t)kTileCap) tlist[p] = (uint32_t)(tid + b * kSelectThreads);
+        }
+        base += (uint32_t)__popcll(qm[b]);
+      }
     }
   }
   for (int t = tid + kB * kSelectThreads; t < ntiles; t += kSelectThreads)
@@ -449,36 +493,52 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
       }
     }
   __syncthreads();  // B3
+  stamp(3);
 
   // ---- gather: each thread takes whole qualifying tiles (one latency round when the
   // list has <= 256 tiles): eligibility words and the tile's eight 16-B score loads ----
   auto gather_tile = [&](int t) {
     float4 v[8];
 #pragma unroll
-    for (int c4 = 0; c4 < 8; ++c4) v[c4] = s_quad(t, c4);
-    const uint32_t ok = elig(t);
+    for (int c4 = 0; c4 < 8; ++c4)
+      v[c4] = (ABL & 16) ? make_float4(t * 1e-3f, c4 * 1e-3f, 0.f, 0.f) : s_quad(t, c4);
+    const uint32_t ok = (ABL & 32) ? ~0u : elig(t);
+    uint32_t m = 0;  // items of the tile that become candidates
 #pragma unroll
     for (int c4 = 0; c4 < 8; ++c4) {
       const float f[4] = {v[c4].x, v[c4].y, v[c4].z, v[c4].w};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int it = 4 * c4 + c, j = t * 32 + it;
-        const uint32_t o = ord_of(f[c]);
-        if (j < n && ((ok >> it) & 1u) && o >= T0) {
-          const uint32_t p = atomicAdd(&misc[7], 1u);
-          if (p < kCandCap) cand[p] = make_key(o, a.gid0 + (uint32_t)j);
+        const int it = 4 * c4 + c;
+        m |= (t * 32 + it < n && ((ok >> it) & 1u) && ord_of(f[c]) >= T0) ? (1u << it) : 0u;
+      }
+    }
+    if (!m) return;
+    uint32_t p = atomicAdd(&misc[7], (uint32_t)__popc(m));  // one LDS atomic per tile
+#pragma unroll
+    for (int c4 = 0; c4 < 8; ++c4) {
+      const float f[4] = {v[c4].x, v[c4].y, v[c4].z, v[c4].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int it = 4 * c4 + c;
+        if ((m >> it) & 1u) {
+          if (p < (uint32_t)kCandCap) cand[p] = make_key(ord_of(f[c]), a.gid0 + (uint32_t)(t * 32 + it));
+          ++p;
         }
       }
     }
   };
   const uint32_t ntl = misc[8];
   if (ntl <= (uint32_t)kTileCap) {
-    for (uint32_t i = tid; i < ntl; i += kSelectThreads) gather_tile((int)tlist[i]);
+    // list slot i -> thread (i % 4)·64 + i / 4: a short list spreads over all four waves
+    const uint32_t slot = ((uint32_t)lane << 2) | (uint32_t)wave;
+    for (uint32_t i = slot; i < ntl; i += kSelectThreads) gather_tile((int)tlist[i]);
   } else {  // list overflow (masses of ties at the bound): every tile reaching T0
     for (int t = tid; t < ntiles; t += kSelectThreads)
       if (trow[t] >= T0) gather_tile(t);
   }
   __syncthreads();  // B4
+  stamp(4);
   uint32_t cnt = misc[7];
   if constexpr (ABL == 4) { if (cnt == 0x12345u) a.keys_out[row] = cnt; return; }
   if (cnt > (uint32_t)kCandCap) {
@@ -497,6 +557,11 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     if (cnt <= 64) wave_sort_emit<1>(cand, (int)cnt, a, row, gmax);
     else if (cnt <= 128) wave_sort_emit<2>(cand, (int)cnt, a, row, gmax);
     else wave_sort_emit<4>(cand, (int)cnt, a, row, gmax);
+    if (a.trace && tid == 0) {
+      stamp(5);
+      a.trace[row * 8 + 6] = cnt;
+      a.trace[row * 8 + 7] = misc[8];
+    }
     return;
   }
   int P = 1;

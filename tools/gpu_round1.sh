@@ -4,7 +4,7 @@
 # Every GPU step has its own time limit; the script stops at the first abnormal exit.
 set -u
 R=$(pwd)
-O="$R/gpurun_out/r01"
+O="$R/gpurun_out/${TAG:-r01}"
 mkdir -p "$O/prof" "$O/pmc"
 timeout -k 10 900 python -m pytest tests -q -m gpu -x > "$O/pytest_gpu.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -5 "$O/pytest_gpu.log"

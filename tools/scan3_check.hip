@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../brickbrain-rec-engine_amd/csrc/scan3_kernel.h"
+#include "../brickbrain-rec-engine_amd/csrc/select.hip"
 
 using namespace bb;
 
@@ -231,6 +232,88 @@ int main() {
   if (!trace("no_stage_no_epi", N / 32, scan3_kernel<48, 256 | 3>)) return 1;
   if (!trace("full_k1", chunks, scan3_kernel<48, 256>)) return 1;
   a.trace = nullptr;
+  // ---- select over the blocked scores of one full scan launch (similar-sets shape:
+  // rank-0 drop, K_int = k + 1 = 51): results against a host top-k, timings, timeline ----
+  {
+    hipLaunchKernelGGL((scan3_kernel<48, 0>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32);
+    (void)hipDeviceSynchronize();
+    const int k = 50, Kint = 51;
+    float* osc;
+    int64_t* oid;
+    int32_t* ocnt;
+    uint64_t *keys, *maxk, *sel_tr;
+    (void)hipMalloc(&osc, M * k * 4);
+    (void)hipMalloc(&oid, M * k * 8);
+    (void)hipMalloc(&ocnt, M * 4);
+    (void)hipMalloc(&keys, M * Kint * 8);
+    (void)hipMalloc(&maxk, M * 8);
+    (void)hipMalloc(&sel_tr, M * 8 * 8);
+    SelectArgs sa{};
+    sa.S = dS; sa.lds = N; sa.tmax = tm; sa.pmax = pm; sa.ldt = N / 32; sa.n_cols = N; sa.slab_start = 0;
+    sa.gid0 = 0; sa.present = ones; sa.K = Kint; sa.keys_out = keys; sa.max_inout = maxk; sa.first_slab = 1;
+    sa.out_scores = osc; sa.out_ids = oid; sa.out_counts = ocnt; sa.k_final = k; sa.s_blocked = 1;
+    if (launch_select(sa, M, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess) { printf("{\"select\":\"error\"}\n"); return 1; }
+    (void)hipMemcpy(S.data(), dS, S.size() * 4, hipMemcpyDeviceToHost);
+    auto SV = [&](int i, int j) { return S[sblk_quad(i, j >> 5, (j >> 2) & 7, N / 32) + (j & 3)]; };
+    std::vector<int64_t> ids(M * k);
+    (void)hipMemcpy(ids.data(), oid, ids.size() * 8, hipMemcpyDeviceToHost);
+    long wrong = 0;
+    std::vector<int> ord(N);
+    for (int i = 0; i < M; ++i) {
+      for (int j = 0; j < N; ++j) ord[j] = j;
+      std::partial_sort(ord.begin(), ord.begin() + k + 1, ord.end(), [&](int x, int y) {
+        const float fx = SV(i, x), fy = SV(i, y);
+        return fx > fy || (fx == fy && x < y);
+      });
+      for (int r = 0; r < k; ++r) wrong += ids[i * k + r] != ord[r + 1];  // rank 0 dropped
+    }
+    printf("{\"select_ids_wrong\":%ld}\n", wrong);
+    auto stime = [&](const char* name, auto kern) {
+      for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(kern, dim3(M), dim3(kSelectThreads), 0, 0, sa);
+      hipEvent_t e0, e1;
+      (void)hipEventCreate(&e0);
+      (void)hipEventCreate(&e1);
+      (void)hipEventRecord(e0, 0);
+      for (int w = 0; w < 20; ++w) hipLaunchKernelGGL(kern, dim3(M), dim3(kSelectThreads), 0, 0, sa);
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      printf("{\"select_timing\":\"%s\",\"us\":%.2f}\n", name, ms * 1e3 / 20);
+    };
+    stime("full", select_kernel<0>);
+    stime("loads", select_kernel<1>);
+    stime("bound", select_kernel<2>);
+    stime("gather", select_kernel<4>);
+    // timeline of one launch right behind a scan (as in a search)
+    auto strace = [&](const char* name, auto kern) {
+      sa.trace = sel_tr;
+      (void)hipMemset(sel_tr, 0, M * 64);
+      hipLaunchKernelGGL((scan3_kernel<48, 0>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, N / 32);
+      hipLaunchKernelGGL(kern, dim3(M), dim3(kSelectThreads), 0, 0, sa);
+      (void)hipDeviceSynchronize();
+      std::vector<uint64_t> tr(M * 8);
+      (void)hipMemcpy(tr.data(), sel_tr, tr.size() * 8, hipMemcpyDeviceToHost);
+      uint64_t t0 = ~0ull, t5 = 0;
+      double ph[5] = {0}, cnt = 0, ntl = 0;
+      for (int i = 0; i < M; ++i) {
+        const uint64_t* r = &tr[i * 8];
+        t0 = std::min(t0, r[0]);
+        t5 = std::max(t5, r[5]);
+        for (int p = 0; p < 5; ++p) ph[p] += r[p + 1] > r[p] ? (r[p + 1] - r[p]) * 10.0 : 0.0;
+        cnt += r[6];
+        ntl += r[7];
+      }
+      printf("{\"select_trace\":\"%s\",\"ns_loads_B1\":%.0f,\"ns_bound\":%.0f,\"ns_tiles_B3\":%.0f,\"ns_gather_B4\":%.0f,"
+             "\"ns_sort_emit\":%.0f,\"ns_grid\":%.0f,\"cand\":%.1f,\"tiles\":%.1f}\n",
+             name, ph[0] / M, ph[1] / M, ph[2] / M, ph[3] / M, ph[4] / M, (t5 - t0) * 10.0, cnt / M, ntl / M);
+    };
+    strace("full", select_kernel<0>);
+    strace("no_S_loads", select_kernel<16>);
+    strace("no_elig_loads", select_kernel<32>);
+    strace("no_gather_loads", select_kernel<48>);
+    sa.trace = nullptr;
+  }
   // empty grid (tiles 0: every workgroup returns at once) = launch + gap
   if (!timeit("empty_grid", [&] { hipLaunchKernelGGL((scan3_kernel<48, 0>), dim3(2 * chunks), dim3(256), 0, 0, a, chunks, 0); })) return 1;
   return 0;
