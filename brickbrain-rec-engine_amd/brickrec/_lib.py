@@ -18,11 +18,12 @@ BB_HOST, BB_DEVICE = 0, 1
 BB_MODE_SEMANTIC, BB_MODE_SIMILAR, BB_MODE_CF, BB_MODE_HYBRID = 0, 1, 2, 3
 BB_Q_OUT_KEYS = 1
 BB_Q_NULL_STREAM = 2
+BB_OPT_STREAM, BB_OPT_STREAM_MIN_ITEMS, BB_OPT_WORKSPACE_BYTES = 1, 2, 3
 BB_OK, BB_E_ARG, BB_E_HIP, BB_E_STATE, BB_E_NOMEM = 0, -1, -2, -3, -4
 
 # every entry point include/brickrec.h declares (checked by tests/test_abi.py)
 EXPORTS = ("bb_create", "bb_upload_items", "bb_upload_cf", "bb_upload_attrs", "bb_eval_mask",
-           "bb_search", "bb_key_lens", "bb_finalize", "bb_set_profiling", "bb_get_profile",
+           "bb_search", "bb_key_lens", "bb_finalize", "bb_set_profiling", "bb_get_profile", "bb_set_option",
            "bb_info", "bb_get_rows", "bb_destroy", "bb_last_error", "bb_abi_version")
 
 
@@ -90,6 +91,7 @@ def load() -> C.CDLL:
             "bb_finalize": ([P, C.POINTER(bb_query), P, P, C.c_int32, C.POINTER(bb_result)], C.c_int),
             "bb_set_profiling": ([P, C.c_int32], C.c_int),
             "bb_get_profile": ([P, C.POINTER(bb_profile)], C.c_int),
+            "bb_set_option": ([P, C.c_int32, C.c_int64], C.c_int),
             "bb_info": ([P, C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                          C.POINTER(C.c_int32)], C.c_int),
             "bb_get_rows": ([P, P, C.c_int32, P, C.c_int32], C.c_int),

@@ -355,6 +355,14 @@ class ItemIndex:
             out = (out.astype(np.uint32) << 16).view(np.float32)
         return out
 
+    # ------------------------------------------------------------------ options
+    def set_option(self, option: str, value: int):
+        """Tuning knobs: "stream" (-1 auto / 0 off / 1 on), "stream_min_items", "workspace_bytes"."""
+        code = {"stream": L.BB_OPT_STREAM, "stream_min_items": L.BB_OPT_STREAM_MIN_ITEMS,
+                "workspace_bytes": L.BB_OPT_WORKSPACE_BYTES}[option]
+        with self._mu:
+            L.check(self._lib.bb_set_option(self._h, code, int(value)), "bb_set_option")
+
     # ------------------------------------------------------------------ profiling
     def set_profiling(self, on: bool):
         L.check(self._lib.bb_set_profiling(self._h, int(bool(on))), "bb_set_profiling")

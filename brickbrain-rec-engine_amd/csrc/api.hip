@@ -75,6 +75,8 @@ struct bb_index {
   int dtype = F32;
   int64_t id_offset = 0;
   int64_t ws_cap = 512ll << 20;
+  int stream_opt = -1;                 // BB_OPT_STREAM
+  int64_t stream_min_items = 100000;   // BB_OPT_STREAM_MIN_ITEMS
   hipStream_t stream = nullptr;
   std::mutex mu;
 
@@ -89,6 +91,9 @@ struct bb_index {
 
   // workspace
   DevBuf qn, qcf, S, tmax, keys, maxk, stage_in, out_sc, out_id, out_cnt, tmp;
+  // streaming top-K (large indexes): pilot lists, candidate regions, overflow flag
+  DevBuf pilot, cand, cand_cnt, cand_pmax, ovf;
+  uint32_t* ovf_host = nullptr;  // pinned
 
   bool prof = false;
   struct Pending {
@@ -221,8 +226,10 @@ int bb_destroy(bb_index* x) {
       (void)hipEventDestroy(p.b);
     }
     for (DevBuf* b : {&x->items, &x->items_present, &x->ones, &x->zeros, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S, &x->tmax,
-                      &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp})
+                      &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot,
+                      &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3})
       b->release();
+    if (x->ovf_host) (void)hipHostFree(x->ovf_host);
     (void)hipStreamDestroy(x->stream);
   }
   delete x;
@@ -427,8 +434,13 @@ int bb_eval_mask(bb_index* x, const bb_predicate* p, uint32_t* out_bits, int32_t
 
 int bb_key_lens(const bb_query* q, int32_t* sides, int32_t* k_int) { return side_k_int(q, sides, k_int); }
 
-int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
-  if (!x || !q || !res) return fail(BB_E_ARG, "null argument");
+}  // extern "C"
+
+namespace {
+
+constexpr int kRetrySlab = 1;  // search_locked: a streaming candidate region overflowed
+
+int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_stream) {
   int32_t sides, K_int;
   int rc = side_k_int(q, &sides, &K_int);
   if (rc) return rc;
@@ -447,8 +459,6 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   if (out_keys && (!res->keys || !res->max_keys)) return fail(BB_E_ARG, "BB_Q_OUT_KEYS needs keys/max_keys");
   if (!out_keys && (!res->scores || !res->ids)) return fail(BB_E_ARG, "null result buffers");
 
-  std::lock_guard<std::mutex> lk(x->mu);
-  DeviceGuard g(x->device);
   hipStream_t s = (q->flags & BB_Q_NULL_STREAM) ? (hipStream_t)0 : q->stream ? (hipStream_t)q->stream : x->stream;
   const int where = q->where;
   const int64_t nw = (x->n + 31) / 32;
@@ -508,6 +518,45 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   uint64_t* maxk = (uint64_t*)x->maxk.p;
   // single-list modes (semantic / similar / CF) finish inside the last select launch
   const bool fuse_final = !out_keys && sides == 1;
+
+  // ---- streaming top-K geometry (SURVEY.md §8d C4/C5 scale): a pilot slab of the first
+  // n0 items gives each query an exact top-K_int over the sample, whose last key bounds the
+  // K_int-th score from below; one scan over all items then appends every eligible score
+  // reaching that bound to per-lane regions (~K_int·n/n0 per query) and a candidate select
+  // finishes the exact top-K.  No B×n score slab is written. ----
+  // BB_OPT_STREAM (or the BB_STREAM environment variable, for A/B runs) forces it off / on
+  static const int stream_env = getenv("BB_STREAM") ? atoi(getenv("BB_STREAM")) : -1;
+  const int stream_sel = x->stream_opt >= 0 ? x->stream_opt : stream_env;
+  // (the streaming epilogue lives in the query-resident scan kernels only)
+  auto scan_ok = [&](int kp, bool planes) { return planes ? scan3_supported(128, kp) : gemm_uses_scan(x->dtype, 128, kp); };
+  const bool stream = allow_stream && (stream_sel == 1 || (stream_sel != 0 && x->n >= x->stream_min_items)) &&
+                      (!need_content || scan_ok(x->Dpad, x->items3.p != nullptr)) &&
+                      (!need_cf || scan_ok(x->Rpad, x->cf3.p != nullptr));
+  int64_t n0 = 0;
+  // regions per query and keys per region for a query chunk of bpad rows: ~4x the expected
+  // K_int·n/n0 candidates spread over the regions, plus slack
+  auto stream_geom = [&](int bpad_c, int& regions, int& cap) {
+    regions = 2 * scan_n_chunks(bpad_c, (int)(x->Npad / 32));
+    const double expect = (double)K_int * ((double)x->n / (double)std::min<int64_t>(n0, x->n)) + K_int;
+    cap = (int)round_up((int64_t)(4.0 * expect / regions) + 32, 16);
+  };
+  if (stream) {
+    n0 = std::min<int64_t>(round_up(std::max<int64_t>(x->n / 16, 64ll * K_int), kTileRows), slab);
+    n0 = std::min<int64_t>(n0, x->Npad);
+    size_t need_keys = 0, need_rg = 0;
+    for (int bp : {(int)round_up(std::min<int64_t>(Bc, B), kTileRows), (int)round_up(B - (B - 1) / Bc * Bc, kTileRows)}) {
+      int rg, cap;
+      stream_geom(bp, rg, cap);
+      need_keys = std::max(need_keys, (size_t)bp * rg * cap);
+      need_rg = std::max(need_rg, (size_t)bp * rg);
+    }
+    if ((rc = x->pilot.ensure((size_t)Bc * K_int * 8)) || (rc = x->cand.ensure(need_keys * 8)) ||
+        (rc = x->cand_cnt.ensure(need_rg * 4)) || (rc = x->cand_pmax.ensure(need_rg * 8)) ||
+        (rc = x->ovf.ensure(256)))
+      return rc;
+    if (!x->ovf_host) BB_HIP(hipHostMalloc((void**)&x->ovf_host, 4, hipHostMallocDefault));
+    BB_HIP(hipMemsetAsync(x->ovf.p, 0, 4, s));
+  }
 
   for (int64_t b0 = 0; b0 < B; b0 += Bc) {
     const int bc = (int)std::min<int64_t>(Bc, B - b0);
@@ -569,9 +618,12 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
     for (int side = 0; side < sides; ++side) {
       const bool cf_side = (q->mode == BB_MODE_CF) || (q->mode == BB_MODE_HYBRID && side == 1);
       const bool side_drop = drop && side == 0;
-      for (int64_t sl = 0; sl < n_slabs; ++sl) {
-        const int64_t c0 = sl * slab;
-        const int ncols = (int)std::min<int64_t>(slab, x->n - c0);
+      // stream: pass 0 = the pilot slab [0, n0) -> pilot lists, pass 1 = the streaming scan
+      const int64_t n_pass = stream ? 2 : n_slabs;
+      for (int64_t sl = 0; sl < n_pass; ++sl) {
+        const bool pilot = stream && sl == 0, spass = stream && sl == 1;
+        const int64_t c0 = stream ? 0 : sl * slab;
+        const int ncols = (int)(spass ? x->n : pilot ? std::min<int64_t>(n0, x->n) : std::min<int64_t>(slab, x->n - c0));
         const int ncols_pad = (int)round_up(ncols, kTileRows);
         GemmArgs ga{};
         ga.Q = cf_side ? x->qcf.p : x->qn.p;
@@ -595,6 +647,18 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
         ga.tmax = (uint32_t*)x->tmax.p;
         ga.pmax = (uint32_t*)x->tmax.p + (size_t)Bc * ldt;
         ga.ldt = ldt;
+        int regions = 0, cand_cap = 0;
+        if (spass) {
+          stream_geom(bpad, regions, cand_cap);
+          ga.thr_keys = (const uint64_t*)x->pilot.p;
+          ga.thr_ld = K_int;
+          ga.cand = (uint64_t*)x->cand.p;
+          ga.cand_cnt = (uint32_t*)x->cand_cnt.p;
+          ga.cand_pmax = side_drop ? (uint64_t*)x->cand_pmax.p : nullptr;
+          ga.cand_cap = cand_cap;
+          ga.gid0 = (uint32_t)x->id_offset;
+          if (scan_n_chunks(bpad, ncols_pad / 32) * 2 != regions) return fail(BB_E_STATE, "stream geometry mismatch");
+        }
         if (cf_side ? fuse_f : fuse_c) {
           ga.q_d = cf_side ? x->r : x->d;
           if (!cf_side && gather_c) {
@@ -619,6 +683,28 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
         } else if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(x->dtype, ga, s); }))) {
           return rc;
         }
+        if (spass) {
+          // candidate select: exact top-K_int of the appended candidates of each query
+          CandSelectArgs ca{};
+          ca.cand = ga.cand;
+          ca.cand_cnt = ga.cand_cnt;
+          ca.cand_pmax = ga.cand_pmax;
+          ca.regions = regions;
+          ca.cap = cand_cap;
+          ca.K = K_int;
+          ca.keys_out = keys + (size_t)side * side_keys;
+          ca.max_out = side_drop ? maxk : nullptr;
+          ca.overflow = (uint32_t*)x->ovf.p;
+          if (fuse_final) {
+            ca.out_scores = o_sc + (size_t)b0 * q->k;
+            ca.out_ids = o_id + (size_t)b0 * q->k;
+            ca.out_counts = o_cnt ? o_cnt + b0 : nullptr;
+            ca.k_final = q->k;
+          }
+          if ((rc = timed(x, K_SELECT, s, [&] { return launch_cand_select(ca, bc, s); }))) return rc;
+          final_pp = 0;
+          continue;
+        }
         const int pp = (int)(sl & 1);
         SelectArgs sa{};
         sa.S = (const float*)x->S.p;
@@ -635,11 +721,12 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
         sa.excl_ld = nw;
         sa.K = K_int;
         sa.s_blocked = (cf_side ? s3_f : s3_c) ? 1 : 0;
-        sa.carry_in = sl ? keys + ((size_t)(pp ^ 1) * sides + side) * side_keys : nullptr;
-        sa.keys_out = keys + ((size_t)pp * sides + side) * side_keys;
-        sa.max_inout = side_drop ? maxk : nullptr;
+        sa.carry_in = sl && !stream ? keys + ((size_t)(pp ^ 1) * sides + side) * side_keys : nullptr;
+        sa.keys_out = pilot ? (uint64_t*)x->pilot.p : keys + ((size_t)pp * sides + side) * side_keys;
+        sa.max_inout = side_drop && !pilot ? maxk : nullptr;
+        sa.pmax = sa.max_inout ? ga.pmax : nullptr;
         sa.first_slab = sl == 0;
-        if (fuse_final && sl == n_slabs - 1) {  // single-list mode: select writes the results
+        if (fuse_final && !stream && sl == n_slabs - 1) {  // single-list mode: select writes the results
           sa.out_scores = o_sc + (size_t)b0 * q->k;
           sa.out_ids = o_id + (size_t)b0 * q->k;
           sa.out_counts = o_cnt ? o_cnt + b0 : nullptr;
@@ -680,6 +767,13 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
     fa.n_rows = bc;
     if ((rc = timed(x, K_FIN, s, [&] { return launch_finalize(fa, s); }))) return rc;
   }
+  if (stream) {
+    // a candidate region overflowed (masses of equal scores, a pilot sample unlike the rest):
+    // the caller reruns the search on the exact slab path
+    BB_HIP(hipMemcpyAsync(x->ovf_host, x->ovf.p, 4, hipMemcpyDeviceToHost, s));
+    BB_HIP(hipStreamSynchronize(s));
+    if (*x->ovf_host) return kRetrySlab;
+  }
   if (host_out) {
     BB_HIP(hipMemcpyAsync(res->scores, o_sc, (size_t)B * q->k * 4, hipMemcpyDeviceToHost, s));
     BB_HIP(hipMemcpyAsync(res->ids, o_id, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
@@ -687,6 +781,19 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   }
   if (host_out || where == BB_HOST) BB_HIP(hipStreamSynchronize(s));
   return BB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
+  if (!x || !q || !res) return fail(BB_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  int rc = search_locked(x, q, res, true);
+  if (rc == kRetrySlab) rc = search_locked(x, q, res, false);
+  return rc;
 }
 
 int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint64_t* max_keys, int32_t n_parts,
@@ -732,6 +839,27 @@ int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint
     BB_HIP(hipStreamSynchronize(s));
   }
   return BB_OK;
+}
+
+int bb_set_option(bb_index* x, int32_t option, int64_t value) {
+  if (!x) return fail(BB_E_ARG, "null index");
+  std::lock_guard<std::mutex> lk(x->mu);
+  switch (option) {
+    case BB_OPT_STREAM:
+      if (value < -1 || value > 1) return fail(BB_E_ARG, "BB_OPT_STREAM must be -1, 0 or 1");
+      x->stream_opt = (int)value;
+      return BB_OK;
+    case BB_OPT_STREAM_MIN_ITEMS:
+      if (value < 0) return fail(BB_E_ARG, "BB_OPT_STREAM_MIN_ITEMS must be >= 0");
+      x->stream_min_items = value;
+      return BB_OK;
+    case BB_OPT_WORKSPACE_BYTES:
+      if (value < (1ll << 20)) return fail(BB_E_ARG, "BB_OPT_WORKSPACE_BYTES must be >= 1 MiB");
+      x->ws_cap = value;
+      return BB_OK;
+    default:
+      return fail(BB_E_ARG, "unknown option " + std::to_string(option));
+  }
 }
 
 int bb_set_profiling(bb_index* x, int32_t on) {

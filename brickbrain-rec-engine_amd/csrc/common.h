@@ -60,7 +60,26 @@ struct GemmArgs {
   int32_t q_d;              // real query width (chunks past it read as 0)
   int32_t q_normalize;      // L2-normalise q_src rows
   uint64_t* trace;          // probe builds only (scan3 ABL & 256): per-workgroup timestamps
+  // streaming top-K (scan ABL & kScanStream): no S slab; every eligible score whose order
+  // image reaches the query's bound is appended to a private per-lane candidate region
+  // (query q, item chunk c, lane half h) -> region (q·n_chunks + c)·2 + h of cand_cap keys
+  const uint64_t* thr_keys; // [Mpad][thr_ld] pilot top-K keys: bound = ord of key thr_ld-1
+  int64_t thr_ld;
+  uint64_t* cand;           // [Mpad·n_chunks·2][cand_cap] keys
+  uint32_t* cand_cnt;       // [Mpad·n_chunks·2] appended per region (> cand_cap = overflow)
+  uint64_t* cand_pmax;      // [Mpad·n_chunks·2] rank-0 key per region (present max) or null
+  int32_t cand_cap;
+  uint32_t gid0;            // global id of column 0
 };
+constexpr int kScanStream = 512;  // scan ABL bit: streaming top-K epilogue
+
+// Item chunks of a query-resident scan launch (shared by the launcher and the host code
+// sizing the streaming candidate regions): one workgroup per CU, ~256 workgroups.
+inline int scan_n_chunks(int Mpad, int tiles) {
+  const int n_groups = Mpad / 128;
+  int n_chunks = (256 + n_groups - 1) / n_groups;
+  return n_chunks < tiles ? n_chunks : tiles;
+}
 
 // scan3 query image ("q3f"): the bf16 planes of 32-query wave blocks in the order the scan
 // loads them.  For query row q (wave block q >> 5, row r = q & 31 inside it), plane P and
@@ -116,6 +135,23 @@ struct SelectArgs {
   uint64_t* trace;          // probe builds only: per-workgroup phase timestamps, or null
 };
 
+// Streaming top-K, second stage: per query, the exact top-K (full key order) of the
+// candidates the streaming scan appended to the query's regions.
+struct CandSelectArgs {
+  const uint64_t* cand;      // [B·regions][cap]
+  const uint32_t* cand_cnt;  // [B·regions]
+  const uint64_t* cand_pmax; // [B·regions] rank-0 keys, or null (no rank-0 drop)
+  int32_t regions, cap;      // regions per query, keys per region
+  int32_t K;                 // internal list length (<= kMaxKInt)
+  uint64_t* keys_out;        // [B][K] when out_scores == null
+  uint64_t* max_out;         // [B] rank-0 key (with cand_pmax), or null
+  float* out_scores;         // [B][k_final] single-list modes: final output (rank-0 dropped)
+  int64_t* out_ids;
+  int32_t* out_counts;
+  int32_t k_final;
+  uint32_t* overflow;        // set to 1 when a region overflowed (results of that row invalid)
+};
+
 struct FinalizeArgs {
   const uint64_t* keys;     // [P][sides][B][K_int]
   const uint64_t* max_keys; // [P][B] or null
@@ -167,6 +203,7 @@ int gemm_tile_m(int dtype);
 int gemm_tile_n(int dtype);
 int gemm_tile_k(int dtype);
 hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s);
+hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s);
 hipError_t launch_mask(const MaskArgs& a, hipStream_t s);

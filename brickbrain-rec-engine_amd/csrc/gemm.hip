@@ -49,10 +49,12 @@ static void launch_scan_t(const GemmArgs& a, hipStream_t s) {
   const int n_groups = a.Mpad / (kScanWaves * 32);
   const int tiles = a.Ncols / 32;
   // one workgroup per CU (LDS + VGPR budget): ~256 workgroups, chunks balanced to ±1 tile
-  int n_chunks = (256 + n_groups - 1) / n_groups;
-  n_chunks = n_chunks < tiles ? n_chunks : tiles;
+  const int n_chunks = scan_n_chunks(a.Mpad, tiles);
   static const bool v1 = getenv("BB_SCAN_V1") != nullptr;
-  if (v1 && !a.q_ids && !a.q_src)
+  if (a.cand)
+    hipLaunchKernelGGL((scan2_kernel<T, KU, kScanStream>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
+                       n_chunks, tiles);
+  else if (v1 && !a.q_ids && !a.q_src)
     hipLaunchKernelGGL((scan_kernel<T, KU>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks,
                        tiles);
   else
@@ -90,9 +92,12 @@ template <int KP>
 static void launch_scan3_t(const GemmArgs& a, hipStream_t s) {
   const int n_groups = a.Mpad / (kScanWaves * 32);
   const int tiles = a.Ncols / 32;
-  int n_chunks = (256 + n_groups - 1) / n_groups;
-  n_chunks = n_chunks < tiles ? n_chunks : tiles;
-  hipLaunchKernelGGL((scan3_kernel<KP>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+  const int n_chunks = scan_n_chunks(a.Mpad, tiles);
+  if (a.cand)
+    hipLaunchKernelGGL((scan3_kernel<KP, kScanStream>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
+                       n_chunks, tiles);
+  else
+    hipLaunchKernelGGL((scan3_kernel<KP>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
 }
 
 hipError_t launch_scan3(const GemmArgs& a, hipStream_t s) {
@@ -122,7 +127,8 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   if (gemm_uses_scan(dtype, a.Mpad, a.Kpad)) {
     if (dtype == BF16 ? launch_scan<uint16_t>(a, s) : launch_scan<float>(a, s)) return hipGetLastError();
   }
-  if (a.q_ids || a.q_src) return hipErrorInvalidValue;  // the fused query prologue is scan-only
+  // the fused query prologue and the streaming epilogue are scan-only
+  if (a.q_ids || a.q_src || a.cand) return hipErrorInvalidValue;
   const int blocks = (a.Mpad / bm) * (a.Ncols / bn);
   if (dtype == BF16) {
     constexpr int nt = CfgBF16::WM * CfgBF16::WN * 64;

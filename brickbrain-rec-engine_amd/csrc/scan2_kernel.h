@@ -131,6 +131,72 @@ __device__ __forceinline__ void tile_maxima(const f32x16s& p, int tile0, int n_v
   tp = t;
 }
 
+// Streaming top-K epilogue (ABL & kScanStream) of one half tile (this lane's 16 items).
+// Per lane: the query's bound thr, a private candidate region reg[0..cap) with count n,
+// and the running rank-0 key (present arg-max) rkey with its folded order image rp.
+struct StreamLane {
+  uint32_t thr = 0xFFFFFFFFu;
+  uint32_t n = 0;
+  uint32_t rp = 0;
+  uint64_t rkey = 0;
+  uint64_t* reg = nullptr;
+};
+
+// Append every eligible item whose order image reaches the bound.  Wave-uniform skip when
+// no lane's half-tile maximum reaches it (the common case once the bound is tight).
+__device__ __forceinline__ void stream_append(const f32x16s& p, int tile0, int n_valid, uint32_t ok, int h,
+                                              uint32_t te, StreamLane& s, uint32_t cap, uint32_t gid0) {
+  if (!__any(te >= s.thr)) return;
+  if (te >= s.thr) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int it = (g & 3) + 8 * (g >> 2) + 4 * h;
+      const uint32_t o = ord_of(p[g]);
+      if (tile0 + it < n_valid && ((ok >> it) & 1u) && o >= s.thr) {
+        if (s.n < cap) s.reg[s.n] = make_key(o, gid0 + (uint32_t)(tile0 + it));
+        ++s.n;
+      }
+    }
+  }
+}
+
+// Rank 0 (similar-sets drops the unmasked arg-max, recommendation_system.py:217): a new
+// running present maximum is rare (record values along the scan), so its item is resolved
+// only then — the first present in-range item equal (as a float: -0 == +0, numpy argmax)
+// to the half-tile maximum; later tiles need a strictly larger maximum (lower id wins ties).
+__device__ __forceinline__ void stream_rank0(const f32x16s& p, int tile0, int n_valid, uint32_t pw, int h,
+                                             uint32_t tp, StreamLane& s, uint32_t gid0) {
+  if (!__any(tp > s.rp)) return;
+  if (tp > s.rp) {
+    const float mv = float_of_ord(tp);
+    bool found = false;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int it = (g & 3) + 8 * (g >> 2) + 4 * h;
+      if (!found && tile0 + it < n_valid && ((pw >> it) & 1u) && p[g] == mv) {
+        s.rkey = make_key(ord_of(p[g]), gid0 + (uint32_t)(tile0 + it));
+        found = true;
+      }
+    }
+    s.rp = tp;
+  }
+}
+
+// Per-lane streaming state at kernel start: the query's bound is the order image of the
+// last key of its pilot top-K list (0 = fewer eligible pilot items than K: take every
+// eligible item); padded query rows take nothing.
+__device__ __forceinline__ void stream_begin(const GemmArgs& a, int q, size_t region, StreamLane& s) {
+  s.reg = a.cand + region * (size_t)a.cand_cap;
+  if (q < a.M_valid) {
+    const uint32_t o = ordk_of(a.thr_keys[(size_t)q * a.thr_ld + a.thr_ld - 1]);
+    s.thr = o ? o : 1u;
+  }
+}
+__device__ __forceinline__ void stream_end(const GemmArgs& a, size_t region, const StreamLane& s) {
+  a.cand_cnt[region] = s.n;
+  if (a.cand_pmax) a.cand_pmax[region] = s.rkey;
+}
+
 // ABL (tools/scan_probe only): 1 = no epilogue, 2 = no staging after the first tile,
 // 4 = no per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no
 // order-image / maxima arithmetic.
@@ -213,6 +279,10 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   const size_t w0 = (size_t)(a.slab_start >> 5);
   const uint32_t* erow = a.excl + (size_t)(q < a.M_valid ? q : a.M_valid - 1) * a.excl_ld;
   float* Srow = a.S + (size_t)q * a.lds;
+  constexpr bool STREAM = (ABL & kScanStream) != 0;
+  StreamLane sl;
+  const size_t region = ((size_t)q * n_chunks + chunk) * 2 + h;
+  if constexpr (STREAM) stream_begin(a, q, region, sl);
 
   // first tile
 #pragma unroll
@@ -279,18 +349,24 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
           if constexpr (s == 0) {
             if constexpr (epi && !(ABL & 32)) tile_maxima(p, ptile0, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
           } else if constexpr (s == 1) {
-            if constexpr (epi && !(ABL & 32)) {
+            if constexpr (epi && STREAM) {
+              stream_append(p, ptile0, a.n_valid, pw & mw & ~ew, h, te, sl, (uint32_t)a.cand_cap, a.gid0);
+            } else if constexpr (epi && !(ABL & 32)) {
               const uint32_t te2 = xor32(te), tp2 = xor32(tp);
               te = te2 > te ? te2 : te;
               tp = tp2 > tp ? tp2 : tp;
             }
+          } else if constexpr (s == 2 && STREAM) {
+            if constexpr (epi) {
+              if (a.cand_pmax) stream_rank0(p, ptile0, a.n_valid, pw, h, tp, sl, a.gid0);
+            }
           } else if constexpr (s < 6) {
-            if constexpr (epi && !(ABL & 8)) {
+            if constexpr (epi && !(ABL & 8) && !STREAM) {
               constexpr int j = s - 2;
               *(float4*)(Srow + ptile0 + 8 * j + 4 * h) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
             }
           } else if constexpr (s == 6) {
-            if constexpr (epi && !(ABL & 16)) {
+            if constexpr (epi && !(ABL & 16) && !STREAM) {
               (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
             }
           } else if constexpr (s == 7) {
@@ -322,6 +398,11 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15");  // asm-MFMA result -> VALU read
     uint32_t te = 0, tp = 0;
     tile_maxima(p, tile * 32, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
+    if constexpr (STREAM) {
+      stream_append(p, tile * 32, a.n_valid, pw & mw & ~ew, h, te, sl, (uint32_t)a.cand_cap, a.gid0);
+      if (a.cand_pmax) stream_rank0(p, tile * 32, a.n_valid, pw, h, tp, sl, a.gid0);
+      return;
+    }
     const uint32_t te2 = xor32(te), tp2 = xor32(tp);
     te = te2 > te ? te2 : te;
     tp = tp2 > tp ? tp2 : tp;
@@ -351,6 +432,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     tile_body(B0{}, EY{}, tile, accE, accO);
     ++tile;
   }
+  if constexpr (STREAM) stream_end(a, region, sl);
 }
 
 }  // namespace bb

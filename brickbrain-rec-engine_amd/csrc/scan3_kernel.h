@@ -104,6 +104,10 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
   const uint32_t* erow = a.excl + (size_t)(q < a.M_valid ? q : a.M_valid - 1) * a.excl_ld;
   // blocked score image (sblk_quad): this wave's 4-KiB block per tile, lane-linear
   float* Sblk = a.S + (size_t)(q >> 5) * a.ldt * 1024 + lane * 4;
+  constexpr bool STREAM = (ABL & kScanStream) != 0;
+  StreamLane sl;
+  const size_t region = ((size_t)q * n_chunks + chunk) * 2 + h;
+  if constexpr (STREAM) stream_begin(a, q, region, sl);
 
   // first tile's LDS-DMA ahead of the query loads: both streams are in flight together
   if constexpr (!(ABL & 128)) {
@@ -208,18 +212,24 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
           if constexpr (s == 0) {
             if constexpr (epi && !(ABL & 32)) tile_maxima(p, ptile0, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
           } else if constexpr (s == 1) {
-            if constexpr (epi && !(ABL & 32)) {
+            if constexpr (epi && STREAM) {
+              stream_append(p, ptile0, a.n_valid, pw & mw & ~ew, h, te, sl, (uint32_t)a.cand_cap, a.gid0);
+            } else if constexpr (epi && !(ABL & 32)) {
               const uint32_t te2 = xor32(te), tp2 = xor32(tp);
               te = te2 > te ? te2 : te;
               tp = tp2 > tp ? tp2 : tp;
             }
+          } else if constexpr (s == 2 && STREAM) {
+            if constexpr (epi) {
+              if (a.cand_pmax) stream_rank0(p, ptile0, a.n_valid, pw, h, tp, sl, a.gid0);
+            }
           } else if constexpr (s < 6) {
-            if constexpr (epi && !(ABL & 8)) {
+            if constexpr (epi && !(ABL & 8) && !STREAM) {
               constexpr int j = s - 2;
               *(float4*)(Sblk + (size_t)ptile * 1024 + j * 256) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
             }
           } else if constexpr (s == 6) {
-            if constexpr (epi && !(ABL & 16)) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
+            if constexpr (epi && !(ABL & 16) && !STREAM) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
           } else if constexpr (s == 7) {
             nw_p = a.present[w0 + tile];
             nw_m = a.mask[w0 + tile];
@@ -248,6 +258,11 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15");  // asm-MFMA result -> VALU read
     uint32_t te = 0, tp = 0;
     tile_maxima(p, tile * 32, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
+    if constexpr (STREAM) {
+      stream_append(p, tile * 32, a.n_valid, pw & mw & ~ew, h, te, sl, (uint32_t)a.cand_cap, a.gid0);
+      if (a.cand_pmax) stream_rank0(p, tile * 32, a.n_valid, pw, h, tp, sl, a.gid0);
+      return;
+    }
     const uint32_t te2 = xor32(te), tp2 = xor32(tp);
     te = te2 > te ? te2 : te;
     tp = tp2 > tp ? tp2 : tp;
@@ -279,6 +294,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
     tile_body(B0{}, EY{}, tile, accE, accO);
     ++tile;
   }
+  if constexpr (STREAM) stream_end(a, region, sl);
   if constexpr (ABL & 256) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp(29);

@@ -594,6 +594,159 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   for (int i = tid; i < K; i += kSelectThreads) out[i] = i < (int)cnt ? cand[i] : 0ull;
 }
 
+// ---- streaming top-K, second stage -------------------------------------------------------
+// The K-th largest of n distinct keys (get(i), non-zero) by a 64-bit radix select in six
+// digit passes (12/12/12/12/8/8 bits); 0 when n < K (take every key).
+template <typename Get>
+__device__ uint64_t kth_key(Get get, int n, uint32_t K, uint32_t* hist, uint32_t* misc, uint32_t* scan_sh) {
+  if ((uint32_t)n < K) return 0ull;
+  const int tid = threadIdx.x;
+  uint64_t prefix = 0, pmask = 0;
+  uint32_t need = K;
+#pragma unroll 1
+  for (int pass = 0; pass < 6; ++pass) {
+    const int shift = pass < 4 ? 52 - 12 * pass : 8 * (5 - pass);
+    const int nb = pass < 4 ? 4096 : 256;
+    for (int i = tid; i < nb; i += kSelectThreads) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += kSelectThreads) {
+      const uint64_t key = get(i);
+      if ((key & pmask) == prefix) atomicAdd(&hist[(uint32_t)(key >> shift) & (uint32_t)(nb - 1)], 1u);
+    }
+    __syncthreads();
+    find_bin(hist, nb, need, misc, scan_sh);
+    const uint32_t b = misc[0], above = misc[1];
+    prefix |= (uint64_t)b << shift;
+    pmask |= (uint64_t)(nb - 1) << shift;
+    need -= above;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+constexpr int kCsRegionsMax = 1024;
+constexpr int kCsOffHist = kCandCap * 8;
+constexpr int kCsOffSel = kCsOffHist + 4096 * 4;
+constexpr int kCsOffPre = kCsOffSel + kMaxKInt * 8;
+constexpr int kCsOffMisc = kCsOffPre + (kCsRegionsMax + 1) * 4;
+constexpr int kCsLds = kCsOffMisc + 256;
+
+// One workgroup per query: gather the appended candidates of its regions (LDS when they fit),
+// select the K largest keys exactly, sort them and emit the final list (rank 0 dropped when
+// it heads it) or the key list — the same outputs as select_kernel on a single slab.
+__global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectArgs a) {
+  __shared__ __attribute__((aligned(16))) char dsm[kCsLds];
+  uint64_t* cand = (uint64_t*)dsm;
+  uint32_t* hist = (uint32_t*)(dsm + kCsOffHist);
+  uint64_t* sel = (uint64_t*)(dsm + kCsOffSel);
+  uint32_t* pre = (uint32_t*)(dsm + kCsOffPre);
+  uint32_t* misc = (uint32_t*)(dsm + kCsOffMisc);
+  uint32_t* scan_sh = misc + 16;
+  uint64_t* red = (uint64_t*)(misc + 32);
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int R = a.regions;
+  const size_t rbase = (size_t)row * R;
+
+  // region counts -> exclusive prefix (each thread owns up to 4 consecutive regions)
+  uint32_t c[4], sum = 0, ovf = 0;
+  uint64_t gm = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 4 * tid + j;
+    const uint32_t raw = r < R ? a.cand_cnt[rbase + r] : 0u;
+    ovf |= raw > (uint32_t)a.cap ? 1u : 0u;
+    c[j] = raw < (uint32_t)a.cap ? raw : (uint32_t)a.cap;
+    sum += c[j];
+    if (a.cand_pmax && r < R) {
+      const uint64_t k = a.cand_pmax[rbase + r];
+      gm = k > gm ? k : gm;
+    }
+  }
+  if (__any(ovf) && lane == 0) atomicOr(a.overflow, 1u);
+  uint32_t total;
+  uint32_t off = block_excl_scan(sum, scan_sh, total);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 4 * tid + j;
+    if (r < R) pre[r] = off;
+    off += c[j];
+  }
+  if (tid == 0) pre[R] = total;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t y = __shfl_xor(gm, o);
+    gm = y > gm ? y : gm;
+  }
+  if (lane == 0) red[wave] = gm;
+  __syncthreads();
+  uint64_t gmax = 0;
+  if (a.cand_pmax) {
+#pragma unroll
+    for (int i = 0; i < kSelectThreads / 64; ++i) gmax = red[i] > gmax ? red[i] : gmax;
+    if (a.max_out && tid == 0) a.max_out[row] = gmax;
+  }
+  // candidate i -> region by binary search over the prefix
+  auto global_key = [&](int i) -> uint64_t {
+    int lo = 0, hi = R;  // pre[lo] <= i < pre[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (pre[mid] <= (uint32_t)i) lo = mid;
+      else hi = mid;
+    }
+    return a.cand[(rbase + lo) * (size_t)a.cap + (i - pre[lo])];
+  };
+  const int n = (int)total;
+  const uint64_t* src = nullptr;
+  if (n <= kCandCap) {
+    for (int i = tid; i < n; i += kSelectThreads) cand[i] = global_key(i);
+    __syncthreads();
+    src = cand;
+  }
+  SelectArgs sa{};
+  sa.K = a.K;
+  sa.keys_out = a.keys_out;
+  sa.out_scores = a.out_scores;
+  sa.out_ids = a.out_ids;
+  sa.out_counts = a.out_counts;
+  sa.k_final = a.k_final;
+  const uint64_t drop = a.cand_pmax ? gmax : 0ull;
+  if (src && n <= 256) {
+    if (wave != 0) return;
+    if (n <= 64) wave_sort_emit<1>(src, n, sa, row, drop);
+    else if (n <= 128) wave_sort_emit<2>(src, n, sa, row, drop);
+    else wave_sort_emit<4>(src, n, sa, row, drop);
+    return;
+  }
+  // more than 256: the K-th largest key, then the keys >= it (exactly min(K, n) of them)
+  uint64_t kth;
+  if (src) kth = kth_key([&](int i) { return src[i]; }, n, (uint32_t)a.K, hist, misc, scan_sh);
+  else kth = kth_key(global_key, n, (uint32_t)a.K, hist, misc, scan_sh);
+  if (tid == 0) misc[4] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += kSelectThreads) {
+    const uint64_t key = src ? src[i] : global_key(i);
+    if (key >= kth) {
+      const uint32_t p = atomicAdd(&misc[4], 1u);
+      if (p < (uint32_t)kMaxKInt) sel[p] = key;
+    }
+  }
+  __syncthreads();
+  const int m = (int)min(misc[4], (uint32_t)kMaxKInt);
+  if (wave != 0) return;
+  if (m <= 64) wave_sort_emit<1>(sel, m, sa, row, drop);
+  else if (m <= 128) wave_sort_emit<2>(sel, m, sa, row, drop);
+  else if (m <= 256) wave_sort_emit<4>(sel, m, sa, row, drop);
+  else wave_sort_emit<8>(sel, m, sa, row, drop);
+}
+
+hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s) {
+  if (a.K <= 0 || a.K > kMaxKInt || B <= 0 || a.regions <= 0 || a.regions > kCsRegionsMax || a.cap <= 0 ||
+      !a.cand || !a.cand_cnt || !a.overflow || (!a.out_scores && !a.keys_out))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cand_select_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s) {
   if (a.K <= 0 || a.K > kMaxKInt || B <= 0 || a.n_cols <= 0 || !a.tmax || (a.max_inout && !a.pmax) ||
       (a.slab_start & 31))

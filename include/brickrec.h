@@ -182,6 +182,18 @@ typedef struct {
 int bb_set_profiling(bb_index* idx, int32_t on);
 int bb_get_profile(bb_index* idx, bb_profile* out);
 
+/* Search-path options (no reference counterpart: tuning knobs of this implementation).
+ *   BB_OPT_STREAM           -1 auto (default), 0 never, 1 always: the streaming top-K for
+ *                           large indexes (pilot bound + candidate regions, no B×n score
+ *                           slab); auto = when the index has >= BB_OPT_STREAM_MIN_ITEMS rows.
+ *                           Results are identical either way.
+ *   BB_OPT_STREAM_MIN_ITEMS rows from which auto streams (default 100000)
+ *   BB_OPT_WORKSPACE_BYTES  score-slab workspace cap (default 512 MiB) */
+#define BB_OPT_STREAM 1
+#define BB_OPT_STREAM_MIN_ITEMS 2
+#define BB_OPT_WORKSPACE_BYTES 3
+int bb_set_option(bb_index* idx, int32_t option, int64_t value);
+
 /* Stored (normalised, index-dtype) item rows of B global ids into out (B×d, row-major;
  * ids outside this index's rows give zero rows).  ids and out live at `where`.  Lets a
  * row-sharded deployment hand the owning shard's row of a liked set to every shard
