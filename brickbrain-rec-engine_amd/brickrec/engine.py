@@ -110,7 +110,10 @@ class ItemIndex:
         bp = bits.ctypes.data if bits is not None else None
         with self._mu:
             if _is_torch(rows):
+                import torch
                 rows = rows.contiguous()
+                # the library converts on its own stream: the rows must be complete first
+                torch.cuda.current_stream(rows.device).synchronize()
                 n, d = rows.shape
                 rc = self._lib.bb_upload_items(self._h, rows.data_ptr(), n, d, _torch_dtype_code(rows),
                                                int(prenormalized), L.BB_DEVICE, bp)
@@ -339,6 +342,7 @@ class ItemIndex:
             dt = torch.float32 if self.dtype == "f32" else torch.bfloat16
             out = torch.empty((int(ids.shape[0]), self.d), dtype=dt, device=ids.device)
             ids = ids.contiguous()
+            torch.cuda.current_stream(ids.device).synchronize()  # read on the library's stream
             with self._mu:
                 L.check(self._lib.bb_get_rows(self._h, ids.data_ptr(), int(ids.shape[0]), out.data_ptr(),
                                               L.BB_DEVICE), "bb_get_rows")

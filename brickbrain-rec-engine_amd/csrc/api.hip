@@ -772,6 +772,29 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // the caller reruns the search on the exact slab path
     BB_HIP(hipMemcpyAsync(x->ovf_host, x->ovf.p, 4, hipMemcpyDeviceToHost, s));
     BB_HIP(hipStreamSynchronize(s));
+    if (*x->ovf_host && getenv("BB_STREAM_DEBUG")) {
+      int rg, cap;
+      const int bpl = (int)round_up(B - (B - 1) / Bc * Bc, kTileRows);
+      stream_geom(bpl, rg, cap);
+      std::vector<uint32_t> cnt((size_t)bpl * rg);
+      BB_HIP(hipMemcpy(cnt.data(), x->cand_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost));
+      uint32_t mx = 0;
+      double sum = 0;
+      size_t over = 0, arg = 0;
+      for (size_t i = 0; i < cnt.size(); ++i) {
+        if (cnt[i] > mx) mx = cnt[i], arg = i;
+        sum += cnt[i];
+        over += cnt[i] > (uint32_t)cap;
+      }
+      std::vector<uint64_t> pk((size_t)bpl * K_int);
+      BB_HIP(hipMemcpy(pk.data(), x->pilot.p, pk.size() * 8, hipMemcpyDeviceToHost));
+      int zero_rows = 0;
+      for (int i = 0; i < bpl; ++i) zero_rows += pk[(size_t)i * K_int + K_int - 1] == 0;
+      fprintf(stderr, "[bb stream] overflow n=%lld n0=%lld K_int=%d bpad=%d regions=%d cap=%d max=%u at region %zu "
+              "(q=%zu) mean=%.1f over=%zu pilot_rows_with_zero_kth=%d key0[K-1]=%016llx\n", (long long)x->n,
+              (long long)n0, K_int, bpl, rg, cap, mx, arg, arg / rg, sum / cnt.size(), over, zero_rows,
+              (unsigned long long)pk[K_int - 1]);
+    }
     if (*x->ovf_host) return kRetrySlab;
   }
   if (host_out) {

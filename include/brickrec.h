@@ -83,7 +83,9 @@ typedef struct {
  * prenormalized != 0.  Zero rows stay zero (score 0), as in sklearn.
  * present_bits (host, ⌈n/32⌉ words, NULL = all): rows that exist in the content item space
  * (feat_matrix rows, WHERE num_parts > 0 at :115); other rows (e.g. sets that only the CF
- * pivot knows) are never returned by the content side and never count as its rank 0. */
+ * pivot knows) are never returned by the content side and never count as its rank 0.
+ * Device-resident rows (where = BB_DEVICE) are read on the index's own stream: the caller
+ * makes them complete first (e.g. synchronises the stream that produced them). */
 int bb_create(const bb_desc* desc, bb_index** out);
 int bb_upload_items(bb_index* idx, const void* rows, int64_t n, int32_t d, int32_t in_dtype,
                     int32_t prenormalized, int32_t where, const uint32_t* present_bits);
@@ -198,7 +200,8 @@ int bb_set_option(bb_index* idx, int32_t option, int64_t value);
  * ids outside this index's rows give zero rows).  ids and out live at `where`.  Lets a
  * row-sharded deployment hand the owning shard's row of a liked set to every shard
  * (SIMILAR / HYBRID queries with q_rows instead of q_items), the sharded analogue of
- * feat_matrix[target_idx] (recommendation_system.py:213).  Synchronous. */
+ * feat_matrix[target_idx] (recommendation_system.py:213).  Synchronous; device ids are
+ * read on the index's own stream, so they must be complete when the call is made. */
 int bb_get_rows(bb_index* idx, const int64_t* ids, int32_t B, void* out, int32_t where);
 
 int bb_info(bb_index* idx, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* r);

@@ -23,10 +23,17 @@ def brickrec():
     return br
 
 
-def _both(idx, mode, k, **kw):
-    """(stream results, slab results) of one search."""
+def _both(idx, mode, k, stream_gemms=None, **kw):
+    """(stream results, slab results) of one search.  stream_gemms: the scan launches the
+    streaming search must take (pilot + stream pass per side and query chunk) — more means a
+    candidate region overflowed and the search silently reran on the slab path."""
     idx.set_option("stream", 1)
+    idx.set_profiling(True)
     a = idx.search(mode, k, **kw)
+    prof = idx.profile()
+    idx.set_profiling(False)
+    if stream_gemms is not None:
+        assert prof["gemm"]["launches"] == stream_gemms, prof
     idx.set_option("stream", 0)
     b = idx.search(mode, k, **kw)
     idx.set_option("stream", -1)
@@ -44,7 +51,7 @@ def test_stream_semantic_f32_vs_oracle(brickrec):
     q = R.unit_rows(B, d, 4321)
     idx = brickrec.ItemIndex(dtype="f32")
     idx.upload_items(x)
-    (sc, ids, cnt), slab = _both(idx, "semantic", k, q_rows=q)
+    (sc, ids, cnt), slab = _both(idx, "semantic", k, stream_gemms=2, q_rows=q)
     _same((sc, ids, cnt), slab)
     assert np.all(cnt == k)
     sim = R.cosine_scores(q, x).astype(np.float64)
@@ -69,7 +76,7 @@ def test_stream_similar_bf16_mask(brickrec):
     qi = rng.choice(n, B, replace=False)
     idx = brickrec.ItemIndex(dtype="bf16")
     idx.upload_items(x)
-    (sc, ids, cnt), slab = _both(idx, "similar", k, q_items=qi, mask=mask)
+    (sc, ids, cnt), slab = _both(idx, "similar", k, stream_gemms=2, q_items=qi, mask=mask)
     _same((sc, ids, cnt), slab)
     assert np.all(cnt == k)
     for i in range(B):
@@ -91,9 +98,9 @@ def test_stream_hybrid_cf_excl(brickrec):
     idx = brickrec.ItemIndex(dtype="f32")
     idx.upload_items(x)
     idx.upload_cf(f)
-    a, b = _both(idx, "hybrid", k, q_items=qi, q_cf=u, mask=mask, excl=excl)
+    a, b = _both(idx, "hybrid", k, stream_gemms=4, q_items=qi, q_cf=u, mask=mask, excl=excl)
     _same(a, b)
-    a, b = _both(idx, "cf", k, q_cf=u, mask=mask, excl=excl)
+    a, b = _both(idx, "cf", k, stream_gemms=2, q_cf=u, mask=mask, excl=excl)
     _same(a, b)
     sc, ids, cnt = a
     for i in range(0, B, 7):
@@ -108,7 +115,8 @@ def test_stream_two_query_chunks(brickrec):
     q = R.unit_rows(B, d, 24)
     idx = brickrec.ItemIndex(dtype="f32")
     idx.upload_items(x)
-    (sc, ids, cnt), slab = _both(idx, "semantic", k, q_rows=q)
+    idx.set_option("workspace_bytes", 400 << 20)  # query chunks of 1024 (+ 76 padded to 128)
+    (sc, ids, cnt), slab = _both(idx, "semantic", k, stream_gemms=4, q_rows=q)
     _same((sc, ids, cnt), slab)
     sim = R.cosine_scores(q[-5:], x).astype(np.float64)
     for j in range(5):
@@ -140,8 +148,46 @@ def test_stream_small_index_forced(brickrec):
     idx = brickrec.ItemIndex(dtype="f32")
     idx.upload_items(x)
     qi = np.arange(B) * 7
-    a, b = _both(idx, "similar", k, q_items=qi)
+    a, b = _both(idx, "similar", k, stream_gemms=2, q_items=qi)
     _same(a, b)
     for i in range(0, B, 9):
         ri, rs = R.similar_sets(x, int(qi[i]), k)
         assert list(a[1][i]) == list(ri)
+
+
+def test_stream_large_bf16_torch_upload(brickrec):
+    """configs[4]-shaped shard (bf16, 384-d, top-100, similar-sets) uploaded straight from a torch tensor
+    into device memory a previous index just released: the upload must see the finished
+    rows (the library converts on its own stream), so the pilot bound is real and the
+    streaming pass finishes without a region overflow; stream == slab exactly, and the
+    scores match an f64 reference over the stored bf16 rows."""
+    import torch
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(77)
+    old = brickrec.ItemIndex(dtype="bf16")
+    y = torch.randn((50000, 384), generator=g, device=dev)
+    old.upload_items(y)
+    old.search("semantic", 10, q_rows=y[:8])
+    old.close()
+    del y, old
+    torch.cuda.empty_cache()
+    n, d, B, k = 400000, 384, 256, 100
+    x = torch.randn((n, d), generator=g, device=dev)
+    x = x / x.norm(dim=1, keepdim=True)
+    idx = brickrec.ItemIndex(dtype="bf16")
+    idx.upload_items(x, prenormalized=True)     # no explicit sync by the caller
+    qi = torch.randperm(n, generator=g, device=dev)[:B]
+    (sc, ids, cnt), slab = _both(idx, "similar", k, stream_gemms=2, q_items=qi)
+    torch.cuda.synchronize()
+    for u, v in zip((sc, ids, cnt), slab):
+        assert torch.equal(u, v)
+    # reference over the stored bf16 rows (exact products, f64 sums); rank 0 = the item itself
+    rows = idx.get_rows(torch.arange(n, device=dev)).double()
+    ref = rows[qi[:32]] @ rows.T
+    ref[torch.arange(32, device=dev), qi[:32]] = -float("inf")
+    rs, ri = torch.topk(ref, k + 1, dim=1)
+    assert torch.max(torch.abs(sc[:32].double() - rs[:, :k])).item() < 1e-5
+    for i in range(32):
+        if (rs[i, k - 1] - rs[i, k]).item() > 1e-5:
+            assert set(ids[i].tolist()) == set(ri[i, :k].tolist())
