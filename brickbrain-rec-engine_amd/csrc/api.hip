@@ -75,6 +75,7 @@ struct bb_index {
   int dtype = F32;
   int64_t id_offset = 0;
   int64_t ws_cap = 512ll << 20;
+  bool ws_set = false;                 // ws_cap set by the caller (desc / BB_OPT_WORKSPACE_BYTES)
   int stream_opt = -1;                 // BB_OPT_STREAM
   int64_t stream_min_items = 100000;   // BB_OPT_STREAM_MIN_ITEMS
   hipStream_t stream = nullptr;
@@ -206,7 +207,7 @@ int bb_create(const bb_desc* desc, bb_index** out) {
   x->device = dev;
   x->dtype = dtype;
   x->id_offset = desc ? desc->id_offset : 0;
-  if (desc && desc->workspace_bytes > 0) x->ws_cap = desc->workspace_bytes;
+  if (desc && desc->workspace_bytes > 0) x->ws_cap = desc->workspace_bytes, x->ws_set = true;
   hipError_t e = hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete x;
@@ -463,17 +464,44 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   const int where = q->where;
   const int64_t nw = (x->n + 31) / 32;
 
+  // query-row padding: 128-query groups, or whole 256-query groups where the bf16 scan
+  // holds 64 queries per wave (scan4_kernel.h) — any query chunk taller than one group
+  const int64_t rq = x->dtype == BF16 && B > kTileRows ? 2 * kTileRows : kTileRows;
+  auto pad_rows = [&](int64_t b) { return round_up(b, b > kTileRows ? rq : kTileRows); };
+  // BB_OPT_STREAM (or the BB_STREAM environment variable, for A/B runs) forces it off / on
+  static const int stream_env = getenv("BB_STREAM") ? atoi(getenv("BB_STREAM")) : -1;
+  const int stream_sel = x->stream_opt >= 0 ? x->stream_opt : stream_env;
+  // (the streaming epilogue lives in the query-resident scan kernels only)
+  auto scan_ok = [&](int kp, bool planes) { return planes ? scan3_supported(128, kp) : gemm_uses_scan(x->dtype, 128, kp); };
+  const bool stream = allow_stream && (stream_sel == 1 || (stream_sel != 0 && x->n >= x->stream_min_items)) &&
+                      (!need_content || scan_ok(x->Dpad, x->items3.p != nullptr)) &&
+                      (!need_cf || scan_ok(x->Rpad, x->cf3.p != nullptr));
+
   // slab / chunk geometry
-  // A slab is as many item columns as the score workspace holds for a query chunk of up to
-  // 1024 queries; queries beyond the chunk loop over the same slabs again.
-  const int64_t Bt = std::min<int64_t>(round_up(B, kTileRows), 1024);
-  const int64_t slab = std::min<int64_t>(
-      x->Npad, std::max<int64_t>(kTileRows, (x->ws_cap / (Bt * 4)) / kTileRows * kTileRows));
+  // Slab path: a slab is as many item columns as the score workspace holds for a query chunk
+  // of up to 1024 queries; queries beyond the chunk loop over the same slabs again.
+  // Streaming path (below): the workspace only holds the pilot slab [0, n0), so query chunks
+  // grow to 8192 rows — every staged item tile then serves that many queries per launch.
+  // Unless the caller capped the workspace, streaming may use up to 4 GiB of it.
+  const int64_t ws = stream && !x->ws_set ? std::max<int64_t>(x->ws_cap, 4ll << 30) : x->ws_cap;
+  int64_t n0 = 0, lds, Bc;
+  if (stream) {
+    const int64_t n0_target =
+        std::min<int64_t>(round_up(std::max<int64_t>(x->n / 16, 64ll * K_int), kTileRows), x->Npad);
+    const int64_t n0_min = std::min<int64_t>(n0_target, 8192);
+    Bc = std::min<int64_t>(pad_rows(B), 8192);
+    while (Bc > rq && Bc * n0_min * 4 > ws) Bc = std::max<int64_t>(rq, Bc / 2 / rq * rq);
+    n0 = std::max<int64_t>(kTileRows, std::min<int64_t>(n0_target, ws / (Bc * 4) / kTileRows * kTileRows));
+    lds = n0;
+  } else {
+    const int64_t Bt = std::min<int64_t>(pad_rows(B), 1024);
+    lds = std::min<int64_t>(x->Npad, std::max<int64_t>(kTileRows, (ws / (Bt * 4)) / kTileRows * kTileRows));
+    Bc = std::max<int64_t>(rq, (ws / (lds * 4)) / rq * rq);
+    Bc = std::min<int64_t>(Bc, pad_rows(B));
+  }
+  const int64_t slab = lds;        // multiple of kTileRows
   const int64_t n_slabs = (x->n + slab - 1) / slab;
-  const int64_t lds = slab;        // multiple of kTileRows
   const int64_t ldt = slab / 32;   // per-tile maxima per query row
-  int64_t Bc = std::max<int64_t>(kTileRows, (x->ws_cap / (lds * 4)) / kTileRows * kTileRows);
-  Bc = std::min<int64_t>(Bc, round_up(B, kTileRows));
 
   // stage host inputs
   const size_t es_q = elem_size(q->q_dtype), es_cf = elem_size(q->q_cf_dtype);
@@ -524,27 +552,16 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   // K_int-th score from below; one scan over all items then appends every eligible score
   // reaching that bound to per-lane regions (~K_int·n/n0 per query) and a candidate select
   // finishes the exact top-K.  No B×n score slab is written. ----
-  // BB_OPT_STREAM (or the BB_STREAM environment variable, for A/B runs) forces it off / on
-  static const int stream_env = getenv("BB_STREAM") ? atoi(getenv("BB_STREAM")) : -1;
-  const int stream_sel = x->stream_opt >= 0 ? x->stream_opt : stream_env;
-  // (the streaming epilogue lives in the query-resident scan kernels only)
-  auto scan_ok = [&](int kp, bool planes) { return planes ? scan3_supported(128, kp) : gemm_uses_scan(x->dtype, 128, kp); };
-  const bool stream = allow_stream && (stream_sel == 1 || (stream_sel != 0 && x->n >= x->stream_min_items)) &&
-                      (!need_content || scan_ok(x->Dpad, x->items3.p != nullptr)) &&
-                      (!need_cf || scan_ok(x->Rpad, x->cf3.p != nullptr));
-  int64_t n0 = 0;
   // regions per query and keys per region for a query chunk of bpad rows: ~4x the expected
   // K_int·n/n0 candidates spread over the regions, plus slack
   auto stream_geom = [&](int bpad_c, int& regions, int& cap) {
-    regions = 2 * scan_n_chunks(bpad_c, (int)(x->Npad / 32));
+    regions = 2 * scan_chunks(x->dtype, bpad_c, (int)(x->Npad / 32), false);
     const double expect = (double)K_int * ((double)x->n / (double)std::min<int64_t>(n0, x->n)) + K_int;
     cap = (int)round_up((int64_t)(4.0 * expect / regions) + 32, 16);
   };
   if (stream) {
-    n0 = std::min<int64_t>(round_up(std::max<int64_t>(x->n / 16, 64ll * K_int), kTileRows), slab);
-    n0 = std::min<int64_t>(n0, x->Npad);
     size_t need_keys = 0, need_rg = 0;
-    for (int bp : {(int)round_up(std::min<int64_t>(Bc, B), kTileRows), (int)round_up(B - (B - 1) / Bc * Bc, kTileRows)}) {
+    for (int bp : {(int)pad_rows(std::min<int64_t>(Bc, B)), (int)pad_rows(B - (B - 1) / Bc * Bc)}) {
       int rg, cap;
       stream_geom(bp, rg, cap);
       need_keys = std::max(need_keys, (size_t)bp * rg * cap);
@@ -560,7 +577,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
 
   for (int64_t b0 = 0; b0 < B; b0 += Bc) {
     const int bc = (int)std::min<int64_t>(Bc, B - b0);
-    const int bpad = (int)round_up(bc, kTileRows);
+    const int bpad = (int)pad_rows(bc);
     // ---- query prep: fused into the scan kernel's prologue when it runs (gathered item
     // rows; raw f32 rows with 16-B rows), otherwise a prep launch fills qn / qcf ----
     // split-precision scan (f32 index with bf16 planes): queries always come from a prep
@@ -657,7 +674,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           ga.cand_pmax = side_drop ? (uint64_t*)x->cand_pmax.p : nullptr;
           ga.cand_cap = cand_cap;
           ga.gid0 = (uint32_t)x->id_offset;
-          if (scan_n_chunks(bpad, ncols_pad / 32) * 2 != regions) return fail(BB_E_STATE, "stream geometry mismatch");
+          if (scan_chunks(x->dtype, bpad, ncols_pad / 32, false) * 2 != regions)
+            return fail(BB_E_STATE, "stream geometry mismatch");
         }
         if (cf_side ? fuse_f : fuse_c) {
           ga.q_d = cf_side ? x->r : x->d;
@@ -720,7 +738,9 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         sa.excl = cf_side && d_excl ? (const uint32_t*)d_excl + (size_t)b0 * nw : nullptr;
         sa.excl_ld = nw;
         sa.K = K_int;
-        sa.s_blocked = (cf_side ? s3_f : s3_c) ? 1 : 0;
+        // blocked score image: the split scan, and the bf16 scan with 64 queries per wave
+        sa.s_blocked = ((cf_side ? s3_f : s3_c) ||
+                        ((cf_side ? scan_f : scan_c) && scan4_used(x->dtype, bpad))) ? 1 : 0;
         sa.carry_in = sl && !stream ? keys + ((size_t)(pp ^ 1) * sides + side) * side_keys : nullptr;
         sa.keys_out = pilot ? (uint64_t*)x->pilot.p : keys + ((size_t)pp * sides + side) * side_keys;
         sa.max_inout = side_drop && !pilot ? maxk : nullptr;
@@ -774,7 +794,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     BB_HIP(hipStreamSynchronize(s));
     if (*x->ovf_host && getenv("BB_STREAM_DEBUG")) {
       int rg, cap;
-      const int bpl = (int)round_up(B - (B - 1) / Bc * Bc, kTileRows);
+      const int bpl = (int)pad_rows(B - (B - 1) / Bc * Bc);
       stream_geom(bpl, rg, cap);
       std::vector<uint32_t> cnt((size_t)bpl * rg);
       BB_HIP(hipMemcpy(cnt.data(), x->cand_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost));
@@ -879,6 +899,7 @@ int bb_set_option(bb_index* x, int32_t option, int64_t value) {
     case BB_OPT_WORKSPACE_BYTES:
       if (value < (1ll << 20)) return fail(BB_E_ARG, "BB_OPT_WORKSPACE_BYTES must be >= 1 MiB");
       x->ws_cap = value;
+      x->ws_set = true;
       return BB_OK;
     default:
       return fail(BB_E_ARG, "unknown option " + std::to_string(option));

@@ -197,6 +197,10 @@ struct MaskArgs {
 hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s);
 bool gemm_uses_scan(int dtype, int Mpad, int Kpad);  // the query-resident scan kernel runs
 bool scan3_supported(int Mpad, int Kpad);            // split-bf16 scan for an f32 index
+bool scan4_used(int dtype, int Mpad);                // bf16 scan with 64 queries per wave
+// item chunks (candidate regions / 2 per query) of the scan launch for these shapes
+int scan_chunks(int dtype, int Mpad, int tiles, bool split);
+bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s);  // scan4_used(BF16, a.Mpad) shapes
 hipError_t launch_scan3(const GemmArgs& a, hipStream_t s);  // X = item planes, Q = q3f image
 hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t* dst, hipStream_t s);
 int gemm_tile_m(int dtype);

@@ -46,6 +46,12 @@ int gemm_tile_k(int dtype) { return dtype == BF16 ? 64 : 32; }
 
 template <typename T, int KU>
 static void launch_scan_t(const GemmArgs& a, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    if (scan4_used(BF16, a.Mpad)) {
+      launch_scan4(a, KU, s);
+      return;
+    }
+  }
   const int n_groups = a.Mpad / (kScanWaves * 32);
   const int tiles = a.Ncols / 32;
   // one workgroup per CU (LDS + VGPR budget): ~256 workgroups, chunks balanced to ±1 tile

@@ -1,0 +1,45 @@
+// scan4.hip — launcher of the 64-queries-per-wave bf16 scan (scan4_kernel.h); its own
+// translation unit so the template instances compile in parallel with gemm.hip.
+#include <cstdlib>
+
+#include "scan4_kernel.h"
+
+namespace bb {
+
+static bool scan4_env_off() {
+  static const bool off = getenv("BB_NO_SCAN4") != nullptr;
+  return off;
+}
+
+// bf16 index, query rows padded to whole 256-query groups: the 64-queries-per-wave scan
+bool scan4_used(int dtype, int Mpad) { return dtype == BF16 && Mpad % kScan4Queries == 0 && !scan4_env_off(); }
+
+int scan_chunks(int dtype, int Mpad, int tiles, bool split) {
+  return !split && scan4_used(dtype, Mpad) ? scan4_n_chunks(Mpad, tiles) : scan_n_chunks(Mpad, tiles);
+}
+
+template <int KU>
+static void launch_t(const GemmArgs& a, hipStream_t s) {
+  const int tiles = a.Ncols / 32;
+  const int n_chunks = scan4_n_chunks(a.Mpad, tiles);
+  const int blocks = a.Mpad / kScan4Queries * n_chunks;
+  if (a.cand)
+    hipLaunchKernelGGL((scan4_kernel<KU, kScanStream>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+  else
+    hipLaunchKernelGGL((scan4_kernel<KU>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+}
+
+bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s) {
+  switch (ku) {
+    case 8: launch_t<8>(a, s); return true;
+    case 16: launch_t<16>(a, s); return true;
+    case 24: launch_t<24>(a, s); return true;
+    case 32: launch_t<32>(a, s); return true;
+    case 48: launch_t<48>(a, s); return true;
+    case 64: launch_t<64>(a, s); return true;
+    case 96: launch_t<96>(a, s); return true;
+    default: return false;
+  }
+}
+
+}  // namespace bb

@@ -1,0 +1,426 @@
+// scan4_kernel.h — bf16 query-resident scan with 64 queries per wave (256 per workgroup).
+//
+// Why: scan2_kernel<bf16> keeps 32 queries per wave (128 per CU), so every 2-byte item
+// element staged into LDS feeds 2·128 flops.  At the bf16 MFMA rate (4,096 flop/clk/CU) that
+// needs 32 B/clk/CU of L2 -> LDS traffic (≈19.7 TB/s chip-wide), more than LDS-DMA sustains
+// (≈17–19 TB/s measured from a shared L2, MI355X_MICROARCH.md "Indexed rows"), and the
+// 1M / 10M-row configs ran at 0.20–0.28 of the bf16 peak.  Holding two
+// 32-query blocks per wave doubles the reuse of every staged tile: 16 B/clk/CU, half the item
+// stream, and twice the MFMA work per barrier.
+//
+// Registers (one wave per SIMD, 512 per lane): the two query blocks take 8·U registers
+// (U = 16-wide k steps; d = 768: 384, d = 384: 192).  The first 256 live in AGPRs, the rest
+// in VGPRs; both are legal MFMA B operands on gfx950.  There is ONE accumulator per block
+// (2 × 16 VGPRs), not the even/odd pair scan2 uses: the tile is two accumulation chains,
+// block A then block B, and each block's epilogue is woven into the OTHER block's chain:
+//   chain A of tile t  <- epilogue of block B of tile t-1, eligibility words of tile t+1,
+//                         LDS-DMA staging of tile t+1
+//   chain B of tile t  <- epilogue of block A of tile t
+// Item fragments are read from LDS once per chain (2 ds_read_b128 per 2 MFMAs, well inside
+// the LDS budget of one read per 32x32x16 gap).
+//
+// Same contract as scan2_kernel.h — LDS tile layout (XOR swizzle), XCD-aware blockIdx ->
+// (query group, item chunk) mapping, tile maxima for the slab select — except that scores
+// go out as scan3's blocked image (sblk_quad: every store a full 1-KiB wave write), or the
+// streaming epilogue (kScanStream) appending candidates to per-lane regions
+// ((q·n_chunks + chunk)·2 + h, one region set per query as before).
+#pragma once
+#include "scan2_kernel.h"
+
+namespace bb {
+
+constexpr int kScan4Queries = kScanWaves * 64;  // queries per workgroup
+
+// Item chunks of a scan4 launch: ~256 workgroups (one per CU).
+inline int scan4_n_chunks(int Mpad, int tiles) {
+  const int n_groups = Mpad / kScan4Queries;
+  const int n_chunks = (256 + n_groups - 1) / n_groups;
+  return n_chunks < tiles ? n_chunks : tiles;
+}
+
+// Streaming state of one query (scan2's StreamLane without the region pointer, which is
+// recomputed on the rare append: at d = 768 every VGPR counts).
+struct Stream4 {
+  uint32_t thr = 0xFFFFFFFFu;
+  float thrf = __builtin_inff();  // the bound as a float: x >= thrf <=> ord(x) >= thr (±0 aside)
+  uint32_t n = 0;
+  uint32_t rp = 0;
+  uint64_t rkey = 0;
+};
+
+// Appends of one half tile.  hits: bit g = accumulator register g is eligible and reaches the
+// bound (built branch-free in the woven slices).  The wave parks its 16 registers in LDS
+// (4 conflict-free 1-KiB writes) and each lane reads back the register of its next hit —
+// a per-lane dynamic index into registers would compile to long compare/select chains,
+// and per-register branches stall the MFMA stream (measured: either took the 1M-row stream
+// pass from 6.1 to ~10-11 ms).  One store per hit; the loop runs as often as the busiest
+// lane has hits (usually once).  A full region keeps counting (cand_select reports the
+// overflow) and its last slot absorbs the extra stores.
+template <int ABL>
+__device__ __forceinline__ void s4_flush(const GemmArgs& a, const f32x16s& p, int tile0, int h, uint32_t hits,
+                                         Stream4& s, size_t region, float* park) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) *(float4*)(park + j * 256 + lane * 4) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+  uint64_t* reg = a.cand + region * (size_t)a.cand_cap;
+  const uint32_t last = (uint32_t)a.cand_cap - 1u;
+  while (__any(hits != 0u)) {
+    if (hits) {
+      const uint32_t g = (uint32_t)__builtin_ctz(hits);
+      hits &= hits - 1u;
+      const float v = park[(g >> 2) * 256 + lane * 4 + (g & 3u)];
+      const uint32_t it = (g & 3u) + 8u * (g >> 2) + 4u * (uint32_t)h;
+      const uint64_t key = make_key(ord_of(v), a.gid0 + (uint32_t)tile0 + it);
+      if constexpr (ABL & 64)
+        s.rkey ^= key;  // probe: everything but the store
+      else
+        reg[s.n < last ? s.n : last] = key;
+      ++s.n;
+    }
+  }
+}
+
+// This lane's eligible registers of a half tile as a 16-bit mask (bit g = register g):
+// in range and set in ok = present ∧ mask ∧ ¬excl.
+__device__ __forceinline__ uint32_t s4_elig16(uint32_t ok, int tile0, int n_valid, int h) {
+  const int rem = n_valid - tile0;
+  const uint32_t inr = rem >= 32 ? 0xFFFFFFFFu : rem <= 0 ? 0u : ((1u << rem) - 1u);
+  const uint32_t w = (ok & inr) >> (4 * h);  // register g <-> item (g & 3) + 8 (g >> 2) + 4h
+  return (w & 0xFu) | ((w >> 4) & 0xF0u) | ((w >> 8) & 0xF00u) | ((w >> 12) & 0xF000u);
+}
+
+// rank 0: as stream_rank0 (scan2_kernel.h)
+__device__ __forceinline__ void s4_rank0(const GemmArgs& a, const f32x16s& p, int tile0, uint32_t pw, int h,
+                                         uint32_t tp, Stream4& s) {
+  if (!__any(tp > s.rp)) return;
+  if (tp > s.rp) {
+    const float mv = float_of_ord(tp);
+    bool found = false;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int it = (g & 3) + 8 * (g >> 2) + 4 * h;
+      if (!found && tile0 + it < a.n_valid && ((pw >> it) & 1u) && p[g] == mv) {
+        s.rkey = make_key(ord_of(p[g]), a.gid0 + (uint32_t)(tile0 + it));
+        found = true;
+      }
+    }
+    s.rp = tp;
+  }
+}
+
+// u-step of a chain on which woven slice s is issued
+constexpr int scan4_at(int s, int U) { return (s + 2 < U) ? s + 2 : U - 1; }
+// chain A: slice s on u-step s (the staging pieces first, then the next tile's words, then
+// block B's epilogue, which starts at u >= 2 because there is at least one piece)
+constexpr int scan4_atA(int s, int U) { return s < U ? s : U - 1; }
+
+// ABL (tools/scan4_probe only): 1 = no epilogue, 2 = no staging after the first tile, 4 = no
+// per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no streaming
+// appends (compares only), 64 = streaming appends without their stores.
+template <int KU, int ABL = 0>
+__global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, int n_chunks, int tiles_total) {
+  typedef uint16_t T;
+  constexpr int U = KU / 2;        // u-steps (one bf16 MFMA each) per tile and block
+  constexpr int ROWB = KU * 16;
+  constexpr int TILE_B = 32 * ROWB;
+  constexpr int G = (KU % 16 == 0) ? 8 : 4;
+  constexpr int PIECES = KU / 8;   // 1 KiB LDS-DMA pieces per wave per tile
+  constexpr int NA = 64;           // query registers (u32x4) that live in AGPRs
+  static_assert(ROWB <= kScanRowMax, "row too wide for the scan kernel");
+  static_assert(KU % 8 == 0, "KU must split into whole 1 KiB pieces per wave");
+  constexpr bool STREAM = (ABL & kScanStream) != 0;
+  // item tile ring, + (streaming) a 4-KiB register parking area per wave for the appends
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_B + (STREAM ? kScanWaves * 4096 : 0)];
+
+  const int n_groups = a.Mpad / kScan4Queries;
+  const int total = n_groups * n_chunks;
+  const int L = blockIdx.x;
+  const int xcd = L & 7, local = L >> 3, q8 = total >> 3, r8 = total & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+  const int chunk = t / n_groups, group = t - chunk * n_groups;
+  const int tile_lo = (int)((int64_t)chunk * tiles_total / n_chunks);
+  const int tile_hi = (int)((int64_t)(chunk + 1) * tiles_total / n_chunks);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int qA = group * kScan4Queries + wave * 64 + r, qB = qA + 32;
+  if (tile_lo >= tile_hi) return;  // uniform per workgroup
+
+  // LDS fragment addresses (scan2 layout: chunk (2u + h) ^ swz(r) of row r) and LDS-DMA
+  // source offsets are recomputed per use (a few VALU in the MFMA shadow) instead of held
+  // in registers: at d = 768 the two query blocks leave 128 VGPRs for everything else
+  const int swz = scan_swz<KU>(r);
+  const int rrow = r * ROWB;
+  const char* Xg = (const char*)a.X;
+  const size_t ldxb = (size_t)a.ldx * sizeof(T);
+  auto soff = [&](int p) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // opaque per use: no hoisted per-piece registers
+    const int mine = (wave * PIECES + p) * 1024 + ln * 16;
+    const int row = mine / ROWB;
+    const int ch = ((mine % ROWB) >> 4) ^ scan_swz<KU>(row);
+    return (size_t)row * ldxb + ch * 16;
+  };
+  const uint32_t lds_base = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+  // inline asm, as in scan2: the compiler's waitcnt pass must not wait for these
+  auto stage_piece = [&](int tile, int buf, int p) __attribute__((always_inline)) {
+    const char* src = Xg + (size_t)tile * 32 * ldxb + soff(p);
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + buf * TILE_B + (wave * PIECES + p) * 1024);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory");
+  };
+
+  // first tile in flight before the query loads
+#pragma unroll
+  for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
+
+  // queries: block A (qA), block B (qB); register j = b·U + u lives in an AGPR iff j < NA
+  u32x4v qv[2 * U];
+  {
+    const char* rowp[2];
+    bool ok[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int q = b ? qB : qA;
+      ok[b] = q < a.M_valid;
+      if (a.q_ids) {  // similar / hybrid: the stored (normalised, padded) item row of the liked set
+        const int64_t lid = ok[b] ? a.q_ids[q] - a.q_id_offset : 0;
+        ok[b] = ok[b] && lid >= 0 && lid < a.q_n_items;
+        rowp[b] = (const char*)a.q_items_base + (size_t)(ok[b] ? lid : 0) * a.ldx * sizeof(T);
+      } else {
+        rowp[b] = (const char*)a.Q + (size_t)(ok[b] ? q : 0) * a.ldq * sizeof(T);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2 * U; ++j) {
+      const int b = j / U, u = j % U;
+      const uint4 v = *(const uint4*)(rowp[b] + (2 * u + h) * 16);
+      qv[j] = ok[b] ? __builtin_bit_cast(u32x4v, v) : u32x4v{0, 0, 0, 0};
+      if (j < NA)
+        asm volatile("" : "+a"(qv[j]));
+      else
+        asm volatile("" : "+v"(qv[j]));
+    }
+  }
+
+  const size_t w0 = (size_t)(a.slab_start >> 5);
+  const uint32_t* erowA = a.excl + (size_t)(qA < a.M_valid ? qA : a.M_valid - 1) * a.excl_ld;
+  const uint32_t* erowB = a.excl + (size_t)(qB < a.M_valid ? qB : a.M_valid - 1) * a.excl_ld;
+  float* park = (float*)(smem + 2 * TILE_B) + wave * 1024;
+  Stream4 slA, slB;
+  auto region = [&](int q) __attribute__((always_inline)) { return ((size_t)q * n_chunks + chunk) * 2 + h; };
+  if constexpr (STREAM) {  // bound = the last key of the query's pilot list (stream_begin)
+    // (an image at or below ord(-inf) takes every finite score: thrf = -inf)
+    if (qA < a.M_valid) {
+      const uint32_t o = ordk_of(a.thr_keys[(size_t)qA * a.thr_ld + a.thr_ld - 1]);
+      slA.thr = o ? o : 1u;
+      slA.thrf = slA.thr <= 0x007FFFFFu ? -__builtin_inff() : float_of_ord(slA.thr);
+    }
+    if (qB < a.M_valid) {
+      const uint32_t o = ordk_of(a.thr_keys[(size_t)qB * a.thr_ld + a.thr_ld - 1]);
+      slB.thr = o ? o : 1u;
+      slB.thrf = slB.thr <= 0x007FFFFFu ? -__builtin_inff() : float_of_ord(slB.thr);
+    }
+  }
+  // eligibility words of the current tile (pw, mw, ewA, ewB) and of the previous tile for
+  // block B's deferred epilogue (ppw, pmw, pewB)
+  uint32_t pw = a.present[w0 + tile_lo], mw = a.mask[w0 + tile_lo], ewA = erowA[w0 + tile_lo],
+           ewB = erowB[w0 + tile_lo];
+  uint32_t ppw = 0, pmw = 0, pewB = 0, nw_p = 0, nw_m = 0, nw_eA = 0, nw_eB = 0;
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // consume every plain load now (no LDS-DMA outstanding): the compiler's own waits for
+  // them would otherwise land behind later staging and wait for it
+  asm volatile("" : "+v"(pw), "+v"(mw), "+v"(ewA), "+v"(ewB));
+  if constexpr (STREAM) asm volatile("" : "+v"(slA.thr), "+v"(slB.thr), "+v"(slA.thrf), "+v"(slB.thrf));
+  asm volatile("s_nop 4");
+
+  f32x16s accA = {}, accB = {};
+
+  // Epilogue of one block's tile, as kEpi small slices woven into the other block's chain
+  // (each a few instructions, so none outgrows an MFMA issue gap):
+  //   0      tile maxima (eligible te, present tp) of this lane's half tile
+  //   slab:  1 cross-half combine, 2..5 the accumulator as four full 1-KiB stores of the
+  //          blocked score image (sblk_quad), 6 the tile-maxima word
+  //   stream: 0 also the wave-uniform "some lane's maximum reaches its bound" flag and the
+  //          lane's 16-bit eligibility; 1..4 compare 4 registers each against the bound
+  //          (branch-free); 5 the appends (s4_flush); 6 rank 0.
+  //   ep: low 16 bits eligibility, high 16 bits registers at or above the bound.
+  auto epi_slice = [&](auto SS, const f32x16s& p, int ptile, uint32_t epw, uint32_t emw, uint32_t eew, int q,
+                       Stream4& sl, uint32_t& te, uint32_t& tp, uint32_t& ep, bool& any) __attribute__((always_inline)) {
+    constexpr int s = decltype(SS)::value;
+    const int ptile0 = ptile * 32;
+    if constexpr (ABL & 1) return;
+    if constexpr (s == 0) {
+      const uint32_t ok = epw & emw & ~eew;
+      tile_maxima(p, ptile0, a.n_valid, epw, ok, h, te, tp);
+      if constexpr (STREAM) {
+        any = __any(te >= sl.thr);
+        ep = s4_elig16(ok, ptile0, a.n_valid, h);
+      }
+    } else if constexpr (STREAM) {
+      if constexpr (s <= 4) {
+        if (any) {
+          uint32_t m = 0;
+#pragma unroll
+          for (int gg = 0; gg < 4; ++gg) {
+            constexpr int g0 = 4 * (s - 1);
+            m |= p[g0 + gg] >= sl.thrf ? 1u << (16 + g0 + gg) : 0u;
+          }
+          ep |= m;
+        }
+      } else if constexpr (s == 5) {
+        if constexpr (!(ABL & 32))
+          if (any) s4_flush<ABL>(a, p, ptile0, h, (ep >> 16) & ep, sl, region(q), park);
+      } else if constexpr (s == 6) {
+        if (a.cand_pmax) s4_rank0(a, p, ptile0, epw, h, tp, sl);
+      }
+    } else {
+      if constexpr (s == 1) {
+        const uint32_t te2 = xor32(te), tp2 = xor32(tp);
+        te = te2 > te ? te2 : te;
+        tp = tp2 > tp ? tp2 : tp;
+      } else if constexpr (s <= 5) {
+        if constexpr (!(ABL & 8)) {
+          constexpr int j = s - 2;
+          float* dst = a.S + (((size_t)(q >> 5) * a.ldt + ptile) * 4 + j) * 256 + lane * 4;
+          *(float4*)dst = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+        }
+      } else if constexpr (s == 6) {
+        if constexpr (!(ABL & 16)) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
+      }
+    }
+  };
+  constexpr int kEpi = 7;
+  // slice placement inside a chain: epilogue slices from u = 2 (after the tie of the other
+  // accumulator), then (chain A) the next tile's words and staging pieces
+  constexpr int kSlicesA = PIECES + 1 + kEpi;
+  // End of a tile: wait for the LDS-DMA of the next tile, not for the epilogue's stores.
+  // vmcnt counts loads, stores and LDS-DMA together in issue order, and every chain issues
+  // its DMAs first, so vmcnt(n) with n = a lower bound of the vector-memory instructions
+  // issued after them (4 word loads; + the 4 score-image stores per finished block on the
+  // slab path) retires the DMAs while the stores drain behind the next tile.  Waiting with
+  // vmcnt(0) exposed the store latency once per tile (2x on the slab path, 1.6x streaming).
+  constexpr bool kStores = !STREAM && !(ABL & (1 | 8));
+
+  // One tile: chain A over buffer BUF (+ block B's epilogue of tile-1 when EPIB), chain B
+  // (+ block A's epilogue of this tile).
+  auto tile_body = [&](auto BUF, auto EPIB, int tile) __attribute__((always_inline)) {
+    constexpr int buf = decltype(BUF)::value;
+    constexpr bool epib = decltype(EPIB)::value;
+    const int stile = tile + 1 < tile_hi ? tile + 1 : tile;  // branch-free staging target
+    const int wtile = stile;                                 // words of the next tile
+    auto frag = [&](int u) __attribute__((always_inline)) {
+      int sw = swz;
+      asm volatile("" : "+v"(sw));  // opaque per use: no hoisted per-u address registers
+      return *(const u32x4v*)(smem + buf * TILE_B + rrow + (((2 * (u % G) + h) ^ sw) << 4) + (u / G) * G * 32);
+    };
+    uint32_t teB = 0, tpB = 0, teA = 0, tpA = 0, epA = 0, epB = 0;
+    bool anyA = false, anyB = false;
+    // 4-slot fragment ring over both chains (step s: block s / U, k-step s % U), prefetch
+    // distance 2; a fragment stays live one step past its MFMA (inline-asm MFMAs are opaque
+    // to hazard tracking: no ds_read may land in registers an in-flight MFMA still reads)
+    u32x4v fq[4];
+    fq[0] = frag(0);
+    fq[1] = frag(1 % U);
+    static_for<2 * U>([&](auto SS) {
+      constexpr int st = decltype(SS)::value;
+      constexpr int b = st / U, u = st % U;
+      if constexpr (st + 2 < 2 * U) fq[(st + 2) % 4] = frag((st + 2) % U);
+      const u32x4v fv = fq[st % 4];
+      f32x16s& c = b ? accB : accA;
+      if constexpr (st < NA) {
+        if constexpr (u == 0)
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[st]));
+        else
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[st]));
+      } else {
+        // VGPR-resident query operand: the s_nop covers a VALU write (a copy the register
+        // allocator may place) -> MFMA read hazard the compiler cannot see through asm
+        if constexpr (u == 0)
+          asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "v"(qv[st]));
+        else
+          asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "v"(qv[st]));
+      }
+      if constexpr (st > 0) asm volatile("" ::"v"(fq[(st + 3) % 4]));
+      // the other block's accumulator: its chain ended >= 2 MFMAs ago; the tie makes every
+      // VALU read of it come after this point, with an extra wait for the MFMA to retire
+      if constexpr (u == 1) {
+        if constexpr (b == 0) {
+          if constexpr (epib) asm volatile("s_nop 15" : "+v"(accB));
+        } else {
+          asm volatile("s_nop 15" : "+v"(accA));
+        }
+      }
+      if constexpr (b == 0) {
+        static_for<kSlicesA>([&](auto SL) {
+          constexpr int s = decltype(SL)::value;
+          if constexpr (scan4_atA(s, U) == u) {
+            if constexpr (s < PIECES) {
+              if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s);
+            } else if constexpr (s == PIECES) {
+              nw_p = a.present[w0 + wtile];
+              nw_m = a.mask[w0 + wtile];
+              nw_eA = erowA[w0 + wtile];
+              nw_eB = erowB[w0 + wtile];
+            } else {
+              if constexpr (epib)
+                epi_slice(std::integral_constant<int, s - PIECES - 1>{}, accB, tile - 1, ppw, pmw, pewB, qB, slB, teB,
+                          tpB, epB, anyB);
+            }
+          }
+        });
+      } else {
+        static_for<kEpi>([&](auto SL) {
+          constexpr int s = decltype(SL)::value;
+          if constexpr (scan4_at(s, U) == u) epi_slice(SL, accA, tile, pw, mw, ewA, qA, slA, teA, tpA, epA, anyA);
+        });
+      }
+    });
+    ppw = pw;
+    pmw = mw;
+    pewB = ewB;
+    if constexpr (!(ABL & 4)) {
+      constexpr int young = 4 + (kStores ? (epib ? 8 : 4) : 0);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(young) : "memory");
+      __syncthreads();
+    }
+    pw = nw_p;
+    mw = nw_m;
+    ewA = nw_eA;
+    ewB = nw_eB;
+    asm volatile("" : "+v"(pw), "+v"(mw), "+v"(ewA), "+v"(ewB));
+  };
+
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using EY = std::integral_constant<bool, true>;
+  using EN = std::integral_constant<bool, false>;
+  tile_body(B0{}, EN{}, tile_lo);
+  int tile = tile_lo + 1;
+  for (;;) {
+    if (tile >= tile_hi) break;
+    tile_body(B1{}, EY{}, tile);
+    ++tile;
+    if (tile >= tile_hi) break;
+    tile_body(B0{}, EY{}, tile);
+    ++tile;
+  }
+  // block B's epilogue of the last tile (not overlapped)
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" : "+v"(accB));
+  {
+    uint32_t te = 0, tp = 0, ep = 0;
+    bool any = false;
+    static_for<kEpi>([&](auto SL) { epi_slice(SL, accB, tile - 1, ppw, pmw, pewB, qB, slB, te, tp, ep, any); });
+  }
+  if constexpr (STREAM) {
+    a.cand_cnt[region(qA)] = slA.n;
+    a.cand_cnt[region(qB)] = slB.n;
+    if (a.cand_pmax) {
+      a.cand_pmax[region(qA)] = slA.rkey;
+      a.cand_pmax[region(qB)] = slB.rkey;
+    }
+  }
+}
+
+}  // namespace bb

@@ -115,8 +115,9 @@ def test_stream_two_query_chunks(brickrec):
     q = R.unit_rows(B, d, 24)
     idx = brickrec.ItemIndex(dtype="f32")
     idx.upload_items(x)
-    idx.set_option("workspace_bytes", 400 << 20)  # query chunks of 1024 (+ 76 padded to 128)
-    (sc, ids, cnt), slab = _both(idx, "semantic", k, stream_gemms=4, q_rows=q)
+    # a 16 MiB workspace cannot hold 1100 pilot rows: query chunks of 512, 512 and 76 (ragged)
+    idx.set_option("workspace_bytes", 16 << 20)
+    (sc, ids, cnt), slab = _both(idx, "semantic", k, stream_gemms=6, q_rows=q)
     _same((sc, ids, cnt), slab)
     sim = R.cosine_scores(q[-5:], x).astype(np.float64)
     for j in range(5):
