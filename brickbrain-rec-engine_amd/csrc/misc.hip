@@ -2,6 +2,8 @@
 // union-blend), hard-constraint predicate masks and item-row conversion (gfx950).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace bb {
 
 __device__ __forceinline__ float load_elem(const void* p, int dtype, size_t i) {
@@ -290,6 +292,101 @@ struct Blend {
   double hv;
 };
 
+// Single-shard fast path (P == 1: each side's key list is already sorted and unique): no
+// serial list walk and no sort network.  Each side's list is sliced in parallel (rank-0
+// drop = skip the head when it is the unmasked arg-max), the union blend looks each id up
+// in the other list, and every blended entry finds its output position as its rank under
+// (h desc, id asc) — O(n²) independent comparisons, n <= 2·k_side, no barriers inside.
+__global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) {
+  __shared__ uint64_t lst[2][kMaxKInt];
+  __shared__ double eh[2 * kMaxKInt];
+  __shared__ uint64_t ek[2 * kMaxKInt];  // order image of eh (the legacy kernel's sort key)
+  __shared__ uint32_t eg[2 * kMaxKInt];
+  __shared__ int nnz[2], n_ent;
+  const int q = blockIdx.x, tid = threadIdx.x;
+  if (tid < 2) nnz[tid] = 0;
+  if (tid == 0) n_ent = 0;
+  __syncthreads();
+  int cnt_local[2] = {0, 0};
+  for (int side = 0; side < a.sides; ++side)
+    for (int i = tid; i < a.K_int; i += kFinThreads) {
+      const uint64_t key = a.keys[((size_t)side * a.B + q) * a.K_int + i];
+      lst[side][i] = key;
+      cnt_local[side] += key != 0ull;
+    }
+  for (int side = 0; side < a.sides; ++side)
+    if (cnt_local[side]) atomicAdd(&nnz[side], cnt_local[side]);
+  __syncthreads();
+  int start[2] = {0, 0}, c[2] = {0, 0};
+  for (int side = 0; side < a.sides; ++side) {
+    const uint64_t head = lst[side][0];
+    if (side == 0 && a.drop_rank0 && a.max_keys && head && head == a.max_keys[q]) start[side] = 1;
+    const int target = a.hybrid ? a.k_side : a.k;
+    const int avail = nnz[side] - start[side];
+    c[side] = avail < target ? (avail > 0 ? avail : 0) : target;
+  }
+  float* sc = a.scores + (size_t)q * a.k;
+  int64_t* id = a.ids + (size_t)q * a.k;
+  if (!a.hybrid || c[0] == 0 || c[1] == 0) {
+    const int side = (!a.hybrid || c[0] > 0) ? 0 : 1;
+    const int n = c[side] < a.k ? c[side] : a.k;
+    for (int i = tid; i < a.k; i += kFinThreads) {
+      if (i < n) {
+        const uint64_t key = lst[side][start[side] + i];
+        sc[i] = float_of_ord(ordk_of(key));
+        id[i] = (int64_t)gid_of(key);
+      } else {
+        sc[i] = 0.f;
+        id[i] = -1;
+      }
+    }
+    if (a.counts && tid == 0) a.counts[q] = n;
+    return;
+  }
+  // union blend (recommendation_system.py:789-843): content entries, then CF-only entries
+  const uint64_t* L0 = lst[0] + start[0];
+  const uint64_t* L1 = lst[1] + start[1];
+  for (int i = tid; i < c[0]; i += kFinThreads) {
+    const uint32_t g = gid_of(L0[i]);
+    int hit = -1;
+    for (int j = 0; j < c[1]; ++j) hit = gid_of(L1[j]) == g ? j : hit;
+    const double cs = (double)float_of_ord(ordk_of(L0[i]));
+    const double fs = hit >= 0 ? (double)float_of_ord(ordk_of(L1[hit])) : 0.0;
+    eh[i] = a.w_content * cs + a.w_cf * fs;
+    ek[i] = ord64_of(eh[i]);
+    eg[i] = g;
+  }
+  for (int j = tid; j < c[1]; j += kFinThreads) {
+    const uint32_t g = gid_of(L1[j]);
+    bool in_c = false;
+    for (int i = 0; i < c[0]; ++i) in_c |= gid_of(L0[i]) == g;
+    if (!in_c) {
+      const int pos = c[0] + atomicAdd(&n_ent, 1);
+      eh[pos] = a.w_content * 0.0 + a.w_cf * (double)float_of_ord(ordk_of(L1[j]));
+      ek[pos] = ord64_of(eh[pos]);
+      eg[pos] = g;
+    }
+  }
+  __syncthreads();
+  const int ne = c[0] + n_ent;
+  const int n = ne < a.k ? ne : a.k;
+  for (int e = tid; e < ne; e += kFinThreads) {
+    const uint64_t hk = ek[e];
+    const uint32_t g = eg[e];
+    int rank = 0;
+    for (int f = 0; f < ne; ++f) rank += (ek[f] > hk) || (ek[f] == hk && eg[f] < g);
+    if (rank < a.k) {
+      sc[rank] = (float)eh[e];
+      id[rank] = (int64_t)g;
+    }
+  }
+  for (int i = n + tid; i < a.k; i += kFinThreads) {
+    sc[i] = 0.f;
+    id[i] = -1;
+  }
+  if (a.counts && tid == 0) a.counts[q] = n;
+}
+
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
   __shared__ uint64_t buf[kFinMerge];
   __shared__ uint64_t lists[2][kMaxKInt];
@@ -406,7 +503,11 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
   if (a.n_rows > a.B || a.P * a.K_int > kFinMerge || a.K_int > kMaxKInt || a.sides < 1 || a.sides > 2) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(finalize_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
+  static const bool legacy = getenv("BB_FINALIZE_LEGACY") != nullptr;
+  if (a.P == 1 && !legacy)
+    hipLaunchKernelGGL(finalize1_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(finalize_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
   return hipGetLastError();
 }
 
