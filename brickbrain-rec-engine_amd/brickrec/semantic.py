@@ -12,6 +12,14 @@ The reference works like this:
 ``bb_search`` in SEMANTIC mode, for one query or a whole batch. Steps 3-4 stay host code,
 unchanged.
 
+``search_recommendations`` is the drop-in for ``HuggingFaceNLPRecommender.search_recommendations``
+(hf_nlp_recommender.py:1207-1259).  The reference encodes the semantic query and then ignores
+the embedding (``_query_vector_database`` runs ``ORDER BY RANDOM()``, :1310-1349); here the
+embedding drives an exact cosine KNN over the same candidate rows (num_parts > 50, year >=
+2005) — new, documented behaviour — and ``relevance_score`` is the cosine instead of the
+constant 0.8.  The theme branch (:1226-1237, ``_query_by_themes`` :1261-1305) and
+``_apply_filters`` (:1351-1386) are restated as host code over the metadata.
+
 The query encoder is out of scope: its weights are fetched by name and there is no network
 here. Callers pass query vectors, or an ``encoder`` callable that produces them.
 """
@@ -59,6 +67,27 @@ def apply_filters(docs: Sequence[Dict], filters: Optional[Dict]) -> List[Dict]:
         if filters.get("min_age") and m["year"] < 2010:
             continue
         out.append(m)
+    return out
+
+
+def hf_apply_filters(results: Sequence[Dict], filters: Optional[Dict]) -> List[Dict]:
+    """``HuggingFaceNLPRecommender._apply_filters`` (hf_nlp_recommender.py:1351-1386): exact
+    theme-name membership, piece bounds, age bounds when the row carries them."""
+    if not filters:
+        return list(results)
+    out = []
+    for r in results:
+        if filters.get("themes") and r.get("theme") and r["theme"] not in filters["themes"]:
+            continue
+        if filters.get("min_pieces") and r.get("num_parts") and r["num_parts"] < filters["min_pieces"]:
+            continue
+        if filters.get("max_pieces") and r.get("num_parts") and r["num_parts"] > filters["max_pieces"]:
+            continue
+        if filters.get("min_age") and r.get("min_age") and r["min_age"] > filters["min_age"]:
+            continue
+        if filters.get("max_age") and r.get("max_age") and r["max_age"] < filters["max_age"]:
+            continue
+        out.append(r)
     return out
 
 
@@ -116,3 +145,52 @@ class SemanticIndex:
                         "num_parts": m.get("num_parts"), "theme": m.get("theme"),
                         "description": m.get("description", ""), "score": m.get("score", 0.0)})
         return out
+
+    def _hf_row(self, i: int, relevance: float) -> Dict:
+        m = self.metadata[i]
+        return {"set_num": m["set_num"], "name": m.get("name"), "year": m.get("year"),
+                "num_parts": m.get("num_parts"), "theme": m.get("theme") or "Generic",
+                "theme_id": m.get("theme_id"), "img_url": m.get("img_url"), "relevance_score": relevance}
+
+    def search_recommendations(self, processed_query: Dict, top_k: int = 10,
+                               encoder: Optional[Callable[[str], np.ndarray]] = None) -> List[Dict]:
+        """``HuggingFaceNLPRecommender.search_recommendations`` (hf_nlp_recommender.py:1207-1259).
+
+        ``processed_query`` is the reference's ``process_natural_language_query`` result
+        (``semantic_query``, ``filters``, ``confidence``, ``intent``), optionally with a
+        precomputed ``embedding``.  Errors return ``[]`` as the reference does (:1257-1259);
+        so does a text query with no encoder (the reference's "embedding model not
+        available" branch, :1219-1221)."""
+        try:
+            filters = processed_query.get("filters", {}) or {}
+            themes = filters.get("themes", [])
+            if themes:  # _query_by_themes (:1261-1305): LIKE %theme%, parts > 50, year >= 2000
+                pats = [t.lower() for t in themes]
+                rows = [i for i, m in enumerate(self.metadata)
+                        if (m.get("num_parts") or 0) > 50 and (m.get("year") or 0) >= 2000
+                        and any(p in (m.get("theme") or "").lower() for p in pats)]
+                rows.sort(key=lambda i: (-(self.metadata[i].get("num_parts") or 0), -(self.metadata[i].get("year") or 0)))
+                results = [self._hf_row(i, 0.9) for i in rows[: top_k * 2]]
+                if results:
+                    out = hf_apply_filters(results, filters)
+                    for r in out:
+                        r["confidence"] = processed_query["confidence"]
+                        r["intent"] = processed_query["intent"]
+                        r["relevance_score"] = 0.9
+                    return out[:top_k]
+            q = processed_query.get("embedding")
+            if q is None:
+                if encoder is None:
+                    return []
+                q = encoder(processed_query["semantic_query"])
+            # _query_vector_database's candidate rows (:1316-1327), ranked by cosine
+            ok = np.array([(m.get("num_parts") or 0) > 50 and (m.get("year") or 0) >= 2005 for m in self.metadata])
+            sc, ids, cnt = self.search_vectors(np.asarray(q, np.float32), top_k, mask=ok)
+            results = [self._hf_row(int(i), float(v)) for i, v in zip(ids[0][: int(cnt[0])], sc[0][: int(cnt[0])])]
+            out = hf_apply_filters(results, filters)
+            for r in out:
+                r["confidence"] = processed_query["confidence"]
+                r["intent"] = processed_query["intent"]
+            return out[:top_k]
+        except Exception:
+            return []

@@ -55,3 +55,31 @@ def test_read_faiss_flat(tmp_path, golden):
     (tmp_path / "bad").write_bytes(b"nope" + bytes(40))
     with pytest.raises(ValueError):
         read_faiss_flat(str(tmp_path / "bad"))
+
+
+def test_hf_search_recommendations(golden):
+    """HuggingFaceNLPRecommender.search_recommendations drop-in: theme branch (LIKE, parts >
+    50, year >= 2000, parts desc), the KNN branch over the reference's candidate rows
+    (parts > 50, year >= 2005), _apply_filters, confidence/intent, [] without an encoder."""
+    from brickrec.semantic import hf_apply_filters
+    idx, g, names = _index(golden)
+    pq = {"semantic_query": "star wars ship", "filters": {"themes": ["Star Wars"]}, "confidence": 0.7,
+          "intent": "search"}
+    res = idx.search_recommendations(pq, top_k=3)
+    assert len(res) == 3 and all(r["theme"] == "Star Wars" and r["relevance_score"] == 0.9 for r in res)
+    assert [r["num_parts"] for r in res] == sorted((r["num_parts"] for r in res), reverse=True)
+    assert all(r["confidence"] == 0.7 and r["intent"] == "search" for r in res)
+    q = g["vectors"][names.index("75192-1")]
+    pq = {"semantic_query": "x", "filters": {}, "confidence": 0.5, "intent": "search"}
+    assert idx.search_recommendations(pq, top_k=3) == []          # no encoder: as the reference
+    res = idx.search_recommendations(dict(pq, embedding=q), top_k=3)
+    meta = {m["set_num"]: m for m in idx.metadata}
+    eligible = [s for s in names if meta[s]["num_parts"] > 50 and meta[s]["year"] >= 2005]
+    sims = {s: float(np.dot(q, g["vectors"][names.index(s)])) for s in eligible}
+    want = sorted(eligible, key=lambda s: -sims[s])[:3]
+    assert [r["set_num"] for r in res] == want
+    assert all(abs(r["relevance_score"] - sims[r["set_num"]]) < 1e-5 for r in res)
+    res2 = idx.search_recommendations(pq, top_k=3, encoder=lambda s: q)
+    assert [r["set_num"] for r in res2] == want
+    assert hf_apply_filters([{"theme": "Icons", "num_parts": 10}], {"themes": ["Star Wars"]}) == []
+    assert idx.search_recommendations({"filters": None}, top_k=3) == []  # malformed -> []
