@@ -12,6 +12,13 @@ shard: with --gpus N every rank serves its own batches against 
 replica ("replicas only", weak scaling, no collective on the data path); value = queries
 of all ranks / max-over-ranks wall time.
 
+--workload c4 / c5 runs the large-index configs instead (BASELINE.json configs[3] / [4]):
+1M x 768 bf16, B=4096, top-100 / 10M x 384 bf16, B=8192, top-100, the item rows sharded
+across the ranks (ShardedIndex: local streaming top-K, one RCCL all-gather of the candidate
+keys, bb_finalize merge).  Total items are fixed, so more GPUs means smaller shards
+("scaling": "strong"); value = queries answered per second by the whole job.  These are
+not the default line (configs[1] is, per BASELINE.json's metric) and run only on request.
+
 Launch: python bench.py [--gpus 1 --steps 500 --warmup 50]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
@@ -97,6 +104,120 @@ def cpu_baseline(x_np, q_np, k, budget_s=10.0, max_batches=400):
                       f"(numpy/BLAS restatement, oracle/restatement.py batched_cosine_topk)"}, ids0
 
 
+SHARDED = {  # BASELINE.json configs[3] / configs[4]
+    "c4": dict(n=1_000_000, d=768, B=4096, k=100, cfg="configs[3]: 1M synthetic items x 768-d bf16, batch=4096, "
+                                                      "top-100, item rows sharded, RCCL top-K merge"),
+    "c5": dict(n=10_000_000, d=384, B=8192, k=100, cfg="configs[4]: 10M synthetic items x 384-d bf16, batch=8192, "
+                                                       "top-100, item rows sharded, RCCL top-K merge"),
+}
+
+
+def unit_rows_chunked(n, d, seed, dev, chunk=1 << 20):
+    import torch
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    out = torch.empty((n, d), dtype=torch.float32, device=dev)
+    for i in range(0, n, chunk):
+        x = torch.randn((min(chunk, n - i), d), generator=g, device=dev)
+        out[i:i + x.shape[0]] = x / x.norm(dim=1, keepdim=True)
+    return out
+
+
+def run_sharded(args, rank, world, local, dev):
+    """configs[3] / [4]: row-sharded streaming top-K + RCCL key all-gather + finalize."""
+    import torch
+    import torch.distributed as dist
+    from brickrec.distributed import ShardedIndex
+    c = SHARDED[args.workload]
+    n, d, B, k = c["n"], c["d"], c["B"], c["k"]
+    if world == 1 and not dist.is_initialized():  # one rank: a group of one (no collective traffic)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    sh = ShardedIndex(n, dtype="bf16")
+    x = unit_rows_chunked(sh.hi - sh.lo, d, 1234 + rank, dev)   # this rank's rows only
+    sh.local.upload_items(x, prenormalized=True)
+    del x
+    torch.cuda.empty_cache()
+    q = unit_rows_chunked(B, d, 4321, dev)                      # replicated batch
+
+    def step():
+        return sh.search("semantic", k, q_rows=q)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lat = []
+    for _ in range(args.steps):
+        t1 = time.perf_counter()
+        res = step()
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    # dominant kernel (the streaming scan: pilot + stream pass per step), on its own stream
+    sh.local.set_profiling(True)
+    ps = max(1, min(args.steps, 5))
+    for _ in range(ps):
+        step()
+    torch.cuda.synchronize()
+    prof = sh.local.profile()
+    sh.local.set_profiling(False)
+    n_loc = sh.hi - sh.lo
+    gemm_us = 1e3 * prof["gemm"]["ms"] / ps                     # per step (all scan launches)
+    flops_loc = 2.0 * B * n_loc * d
+    achieved = flops_loc / (gemm_us * 1e-6) / 1e12
+    alg_bytes = n_loc * d * 2 + B * d * 4 + B * k * 8
+    out = {
+        "metric": f"similarity queries/sec + p50 latency, {d}-d x {n:,} items ({c['cfg'].split(':')[0]})",
+        "value": round(B * args.steps / el, 1), "unit": "queries/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 4),
+        "p50_ms": round(1e3 * float(np.median(lat)), 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (unit-norm N(0,1) rows, seeds 1234+rank / 4321)",
+        "config": {"workload": c["cfg"], "items": n, "items_per_rank": n_loc, "dim": d, "batch": B, "top_k": k,
+                   "parallelism": f"rows sharded x{world}" if world > 1 else "single"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_DENSE_TF, "unit": "TFLOP/s",
+                     "frac": round(achieved / BF16_DENSE_TF, 4), "traffic": None,
+                     "kernel": "scan4_kernel (pilot slab + streaming pass), per rank",
+                     "kernel_us_per_step": round(gemm_us, 1), "algorithmic_flops_per_step": flops_loc,
+                     "algorithmic_bytes_per_step": alg_bytes},
+        "kernels_us_per_step": {kk: round(1e3 * v["ms"] / ps, 2) for kk, v in prof.items() if v["launches"]},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # bounded sample: 64 queries against the first 200K rows, scaled to the full index
+        from oracle.restatement import batched_cosine_topk
+        ns = 200_000
+        xs = sh.local.get_rows(torch.arange(ns, device=dev)).float().cpu().numpy()
+        qs = q[:64].cpu().numpy()
+        batched_cosine_topk(xs, qs[:4], k)
+        t1 = time.perf_counter()
+        nb = 0
+        while nb < 20 and time.perf_counter() - t1 < 10.0:
+            batched_cosine_topk(xs, qs, k)
+            nb += 1
+        rate = nb * 64 / (time.perf_counter() - t1) * ns / n
+        try:
+            from threadpoolctl import threadpool_info
+            cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+        except Exception:
+            cores = os.cpu_count() or 1
+        out["cpu_baseline"] = {"value": round(rate, 2), "unit": "queries/s", "cores": int(cores),
+                               "kind": "port",
+                               "sample": f"{nb} batches x 64 queries x {ns} x {d} (numpy/BLAS restatement), "
+                                         f"rate scaled by {ns}/{n} items"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -106,6 +227,8 @@ def main():
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--inflight", type=int, default=3, help="batches in flight per GPU (1 = strictly serial)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
+                    help="c2 = configs[1] (default line); c4 / c5 = the sharded configs[3] / [4]")
     args = ap.parse_args()
 
     import torch
@@ -117,6 +240,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    if args.workload != "c2":
+        return run_sharded(args, rank, world, local, dev)
 
     import brickrec
     B = args.batch
