@@ -110,9 +110,15 @@ __device__ __forceinline__ void s4_rank0(const GemmArgs& a, const f32x16s& p, in
 
 // u-step of a chain on which woven slice s is issued
 constexpr int scan4_at(int s, int U) { return (s + 2 < U) ? s + 2 : U - 1; }
-// chain A: slice s on u-step s (the staging pieces first, then the next tile's words, then
-// block B's epilogue, which starts at u >= 2 because there is at least one piece)
-constexpr int scan4_atA(int s, int U) { return s < U ? s : U - 1; }
+// chain A: block B's epilogue (slices 0..E-1 from u = 2, after the accumulator tie), the
+// next tile's words (slice E), then the LDS-DMA pieces spaced SP u-steps apart (slices
+// E+1..): each DMA holds the wave's issue for ~20+ cycles, and back to back they stalled
+// the MFMA stream (staging cost 14 % of the kernel with pieces on consecutive u-steps).
+constexpr int scan4_atA(int s, int U, int E, int pieces) {
+  const int sp = (U - (E + 3)) / (pieces > 0 ? pieces : 1) > 1 ? (U - (E + 3)) / pieces : 1;
+  const int u = s < E ? s + 2 : s == E ? E + 2 : E + 3 + (s - E - 1) * sp;
+  return u < U ? u : U - 1;
+}
 
 // ABL (tools/scan4_probe only): 1 = no epilogue, 2 = no staging after the first tile, 4 = no
 // per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no streaming
@@ -295,12 +301,8 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, i
   // slice placement inside a chain: epilogue slices from u = 2 (after the tie of the other
   // accumulator), then (chain A) the next tile's words and staging pieces
   constexpr int kSlicesA = PIECES + 1 + kEpi;
-  // End of a tile: wait for the LDS-DMA of the next tile, not for the epilogue's stores.
-  // vmcnt counts loads, stores and LDS-DMA together in issue order, and every chain issues
-  // its DMAs first, so vmcnt(n) with n = a lower bound of the vector-memory instructions
-  // issued after them (4 word loads; + the 4 score-image stores per finished block on the
-  // slab path) retires the DMAs while the stores drain behind the next tile.  Waiting with
-  // vmcnt(0) exposed the store latency once per tile (2x on the slab path, 1.6x streaming).
+  // End of a tile: wait for the LDS-DMA of the next tile, not for block A's score-image
+  // stores issued after it (vmcnt counts loads, stores and LDS-DMA together, in order).
   constexpr bool kStores = !STREAM && !(ABL & (1 | 8));
 
   // One tile: chain A over buffer BUF (+ block B's epilogue of tile-1 when EPIB), chain B
@@ -355,18 +357,16 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, i
       if constexpr (b == 0) {
         static_for<kSlicesA>([&](auto SL) {
           constexpr int s = decltype(SL)::value;
-          if constexpr (scan4_atA(s, U) == u) {
-            if constexpr (s < PIECES) {
-              if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s);
-            } else if constexpr (s == PIECES) {
+          if constexpr (scan4_atA(s, U, kEpi, PIECES) == u) {
+            if constexpr (s < kEpi) {
+              if constexpr (epib) epi_slice(SL, accB, tile - 1, ppw, pmw, pewB, qB, slB, teB, tpB, epB, anyB);
+            } else if constexpr (s == kEpi) {
               nw_p = a.present[w0 + wtile];
               nw_m = a.mask[w0 + wtile];
               nw_eA = erowA[w0 + wtile];
               nw_eB = erowB[w0 + wtile];
             } else {
-              if constexpr (epib)
-                epi_slice(std::integral_constant<int, s - PIECES - 1>{}, accB, tile - 1, ppw, pmw, pewB, qB, slB, teB,
-                          tpB, epB, anyB);
+              if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s - kEpi - 1);
             }
           }
         });
@@ -381,7 +381,8 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, i
     pmw = mw;
     pewB = ewB;
     if constexpr (!(ABL & 4)) {
-      constexpr int young = 4 + (kStores ? (epib ? 8 : 4) : 0);
+      // issued after the last DMA piece: block A's score-image stores (chain B)
+      constexpr int young = kStores ? 4 : 0;
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(young) : "memory");
       __syncthreads();
     }

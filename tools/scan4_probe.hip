@@ -46,7 +46,7 @@ void l2(const GemmArgs& a, hipStream_t s) {
 
 int main() {
   const int M = 4096;
-  for (int cfg = 2; cfg < 3; ++cfg) {
+  for (int cfg = 0; cfg < 3; ++cfg) {
     const int D = cfg == 1 ? 384 : 768;
     const int N = cfg == 2 ? 1048576 : 131072;  // cfg 2: items far beyond the MALL (1.6 GB)
     uint16_t *q, *x;
@@ -104,6 +104,7 @@ int main() {
             {"s4_no_staging", l4<96, 2 | 24>, 0}};  // (scan2 ABL 8|16 still stores the last tile: S is sized for 131072 columns)
     else if (D == 768)
       vs = {{"s4_full", l4<96, 0>, 0}, {"s4_no_stores", l4<96, 24>, 0}, {"s4_no_epi", l4<96, 1>, 0},
+            {"s4_no_stores_nobarrier", l4<96, 24 | 4>, 0}, {"s4_no_stores_nostage_nobarrier", l4<96, 24 | 4 | 2>, 0},
             {"s4_no_staging", l4<96, 2 | 24>, 0}, {"s4_mfma_lds_only", l4<96, 7>, 0},
             {"s4_no_stores_c32", l4<96, 24>, 32}, {"s4_no_stores_c64", l4<96, 24>, 64},
             {"s2_full", l2<96, 0>, 0}, {"s2_no_epi", l2<96, 1>, 0}, {"s2_mfma_lds_only", l2<96, 7>, 0}};
