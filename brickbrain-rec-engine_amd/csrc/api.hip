@@ -16,6 +16,7 @@
 #include "../../include/brickrec.h"
 #include "common.h"
 
+#include <cmath>
 #include <cstdlib>
 
 using namespace bb;
@@ -39,8 +40,9 @@ int fail(int code, const std::string& msg) {
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 size_t elem_size(int dtype) { return dtype == F64 ? 8 : dtype == BF16 ? 2 : 4; }
 
-enum Kfam { K_PREP = 0, K_GEMM = 1, K_SELECT = 2, K_FIN = 3, K_MASK = 4, K_NFAM = 5 };
-const char* kFamNames[K_NFAM] = {"prep", "gemm", "select", "finalize", "mask"};
+// K_RERUN counts searches the streaming path handed back to the slab path (no kernel time)
+enum Kfam { K_PREP = 0, K_GEMM = 1, K_SELECT = 2, K_FIN = 3, K_MASK = 4, K_RERUN = 5, K_NFAM = 6 };
+const char* kFamNames[K_NFAM] = {"prep", "gemm", "select", "finalize", "mask", "rerun"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -78,6 +80,7 @@ struct bb_index {
   bool ws_set = false;                 // ws_cap set by the caller (desc / BB_OPT_WORKSPACE_BYTES)
   int stream_opt = -1;                 // BB_OPT_STREAM
   int64_t stream_min_items = 100000;   // BB_OPT_STREAM_MIN_ITEMS
+  int refine_opt = -1;                 // BB_OPT_STREAM_REFINE
   hipStream_t stream = nullptr;
   std::mutex mu;
 
@@ -94,6 +97,7 @@ struct bb_index {
   DevBuf qn, qcf, S, tmax, keys, maxk, stage_in, out_sc, out_id, out_cnt, tmp;
   // streaming top-K (large indexes): pilot lists, candidate regions, overflow flag
   DevBuf pilot, cand, cand_cnt, cand_pmax, ovf;
+  DevBuf list1, max1;  // two-level streaming: exact top-K_int (+ rank-0 key) of items [0, n1)
   uint32_t* ovf_host = nullptr;  // pinned
 
   bool prof = false;
@@ -227,7 +231,7 @@ int bb_destroy(bb_index* x) {
       (void)hipEventDestroy(p.b);
     }
     for (DevBuf* b : {&x->items, &x->items_present, &x->ones, &x->zeros, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S, &x->tmax,
-                      &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot,
+                      &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
                       &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
@@ -552,21 +556,50 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   // K_int-th score from below; one scan over all items then appends every eligible score
   // reaching that bound to per-lane regions (~K_int·n/n0 per query) and a candidate select
   // finishes the exact top-K.  No B×n score slab is written. ----
+  // Two-level bound (when the pilot is a small sample of the index): pass A streams items
+  // [0, n1) against the pilot bound and a candidate select turns them into the exact
+  // top-K_int of [0, n1); its last key bounds pass B over [n1, n), whose candidates join
+  // that list in the final select.  Expected appends per query drop from K_int·n/n0 to
+  // K_int·(n1/n0 + n/n1), minimal at n1 = sqrt(n·n0): 16 -> 7 K_int at n0 = n/16 (1M rows),
+  // 76 -> 16 K_int at n0 = n/76 (10M rows).  Appends are what the streaming scan pays for.
+  static const int refine_env = getenv("BB_STREAM_REFINE") ? atoi(getenv("BB_STREAM_REFINE")) : 1;
+  // Auto (measured): from n >= 8·n0 on indexes of 500K+ rows with query chunks of 256+
+  // (10M x 384, B=8192: 83 -> 71 ms; 1.25M: 12.4 -> 11.7 ms); on smaller indexes or batches
+  // the extra candidate select costs more than the appends it saves (125K rows: 1.36 ->
+  // 1.45 ms, B=1: +8 %).  BB_OPT_STREAM_REFINE forces it (tests) when n >= 2·n0.
+  const int refine_sel = x->refine_opt >= 0 ? x->refine_opt : (refine_env == 0 ? 0 : -1);
+  const bool refine = stream && refine_sel != 0 && x->n >= 2 * n0 &&
+                      (refine_sel == 1 || (x->n >= 8 * n0 && x->n >= 500000 && Bc >= 256));
+  const int64_t n1 = refine ? std::min<int64_t>(x->Npad - kTileRows,
+                                                std::max<int64_t>(n0, round_up((int64_t)std::sqrt((double)x->n * (double)n0),
+                                                                               kTileRows)))
+                            : x->n;
+  // streaming pass p (0 = A, 1 = B): item range and the appends expected per query
+  auto pass_cols = [&](int p, int64_t& c0, int64_t& nc) {
+    c0 = p == 0 ? 0 : n1;
+    nc = p == 0 ? std::min<int64_t>(n1, x->n) : x->n - n1;
+  };
   // regions per query and keys per region for a query chunk of bpad rows: ~4x the expected
-  // K_int·n/n0 candidates spread over the regions, plus slack
-  auto stream_geom = [&](int bpad_c, int& regions, int& cap) {
-    regions = 2 * scan_chunks(x->dtype, bpad_c, (int)(x->Npad / 32), false);
-    const double expect = (double)K_int * ((double)x->n / (double)std::min<int64_t>(n0, x->n)) + K_int;
+  // candidates spread over the regions, plus slack
+  auto stream_geom = [&](int bpad_c, int p, int& regions, int& cap) {
+    int64_t c0, nc;
+    pass_cols(p, c0, nc);
+    regions = 2 * scan_chunks(x->dtype, bpad_c, (int)(round_up(nc, kTileRows) / 32), false);
+    const double base = p == 0 ? (double)std::min<int64_t>(n0, x->n) : (double)n1;
+    const double expect = (double)K_int * ((double)nc / base) + K_int;
     cap = (int)round_up((int64_t)(4.0 * expect / regions) + 32, 16);
   };
   if (stream) {
     size_t need_keys = 0, need_rg = 0;
-    for (int bp : {(int)pad_rows(std::min<int64_t>(Bc, B)), (int)pad_rows(B - (B - 1) / Bc * Bc)}) {
-      int rg, cap;
-      stream_geom(bp, rg, cap);
-      need_keys = std::max(need_keys, (size_t)bp * rg * cap);
-      need_rg = std::max(need_rg, (size_t)bp * rg);
-    }
+    for (int bp : {(int)pad_rows(std::min<int64_t>(Bc, B)), (int)pad_rows(B - (B - 1) / Bc * Bc)})
+      for (int p = 0; p < (refine ? 2 : 1); ++p) {
+        int rg, cap;
+        stream_geom(bp, p, rg, cap);
+        need_keys = std::max(need_keys, (size_t)bp * rg * cap);
+        need_rg = std::max(need_rg, (size_t)bp * rg);
+      }
+    if (refine && ((rc = x->list1.ensure((size_t)Bc * K_int * 8)) || (rc = x->max1.ensure((size_t)Bc * 8))))
+      return rc;
     if ((rc = x->pilot.ensure((size_t)Bc * K_int * 8)) || (rc = x->cand.ensure(need_keys * 8)) ||
         (rc = x->cand_cnt.ensure(need_rg * 4)) || (rc = x->cand_pmax.ensure(need_rg * 8)) ||
         (rc = x->ovf.ensure(256)))
@@ -636,11 +669,15 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       const bool cf_side = (q->mode == BB_MODE_CF) || (q->mode == BB_MODE_HYBRID && side == 1);
       const bool side_drop = drop && side == 0;
       // stream: pass 0 = the pilot slab [0, n0) -> pilot lists, pass 1 = the streaming scan
-      const int64_t n_pass = stream ? 2 : n_slabs;
+      // (A: [0, n1)), pass 2 with the two-level bound (B: [n1, n))
+      const int64_t n_pass = stream ? (refine ? 3 : 2) : n_slabs;
       for (int64_t sl = 0; sl < n_pass; ++sl) {
-        const bool pilot = stream && sl == 0, spass = stream && sl == 1;
-        const int64_t c0 = stream ? 0 : sl * slab;
-        const int ncols = (int)(spass ? x->n : pilot ? std::min<int64_t>(n0, x->n) : std::min<int64_t>(slab, x->n - c0));
+        const bool pilot = stream && sl == 0, spass = stream && sl >= 1;
+        const int sp = (int)sl - 1;                       // streaming pass index
+        const bool last_spass = spass && sl == n_pass - 1;
+        int64_t c0 = stream ? 0 : sl * slab, nc_s = 0;
+        if (spass) pass_cols(sp, c0, nc_s);
+        const int ncols = (int)(spass ? nc_s : pilot ? std::min<int64_t>(n0, x->n) : std::min<int64_t>(slab, x->n - c0));
         const int ncols_pad = (int)round_up(ncols, kTileRows);
         GemmArgs ga{};
         ga.Q = cf_side ? x->qcf.p : x->qn.p;
@@ -666,14 +703,14 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         ga.ldt = ldt;
         int regions = 0, cand_cap = 0;
         if (spass) {
-          stream_geom(bpad, regions, cand_cap);
-          ga.thr_keys = (const uint64_t*)x->pilot.p;
+          stream_geom(bpad, sp, regions, cand_cap);
+          ga.thr_keys = (const uint64_t*)(sp == 0 ? x->pilot.p : x->list1.p);
           ga.thr_ld = K_int;
           ga.cand = (uint64_t*)x->cand.p;
           ga.cand_cnt = (uint32_t*)x->cand_cnt.p;
           ga.cand_pmax = side_drop ? (uint64_t*)x->cand_pmax.p : nullptr;
           ga.cand_cap = cand_cap;
-          ga.gid0 = (uint32_t)x->id_offset;
+          ga.gid0 = (uint32_t)(x->id_offset + c0);
           if (scan_chunks(x->dtype, bpad, ncols_pad / 32, false) * 2 != regions)
             return fail(BB_E_STATE, "stream geometry mismatch");
         }
@@ -710,9 +747,19 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           ca.regions = regions;
           ca.cap = cand_cap;
           ca.K = K_int;
+          ca.overflow = (uint32_t*)x->ovf.p;
+          if (!last_spass) {  // pass A of the two-level bound: the exact list of [0, n1)
+            ca.keys_out = (uint64_t*)x->list1.p;
+            ca.max_out = side_drop ? (uint64_t*)x->max1.p : nullptr;
+            if ((rc = timed(x, K_SELECT, s, [&] { return launch_cand_select(ca, bc, s); }))) return rc;
+            continue;
+          }
+          if (refine) {
+            ca.carry_in = (const uint64_t*)x->list1.p;
+            ca.max_in = side_drop ? (const uint64_t*)x->max1.p : nullptr;
+          }
           ca.keys_out = keys + (size_t)side * side_keys;
           ca.max_out = side_drop ? maxk : nullptr;
-          ca.overflow = (uint32_t*)x->ovf.p;
           if (fuse_final) {
             ca.out_scores = o_sc + (size_t)b0 * q->k;
             ca.out_ids = o_id + (size_t)b0 * q->k;
@@ -795,7 +842,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     if (*x->ovf_host && getenv("BB_STREAM_DEBUG")) {
       int rg, cap;
       const int bpl = (int)pad_rows(B - (B - 1) / Bc * Bc);
-      stream_geom(bpl, rg, cap);
+      stream_geom(bpl, refine ? 1 : 0, rg, cap);
       std::vector<uint32_t> cnt((size_t)bpl * rg);
       BB_HIP(hipMemcpy(cnt.data(), x->cand_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost));
       uint32_t mx = 0;
@@ -835,7 +882,10 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
   int rc = search_locked(x, q, res, true);
-  if (rc == kRetrySlab) rc = search_locked(x, q, res, false);
+  if (rc == kRetrySlab) {
+    if (x->prof) ++x->launches[K_RERUN];
+    rc = search_locked(x, q, res, false);
+  }
   return rc;
 }
 
@@ -895,6 +945,10 @@ int bb_set_option(bb_index* x, int32_t option, int64_t value) {
     case BB_OPT_STREAM_MIN_ITEMS:
       if (value < 0) return fail(BB_E_ARG, "BB_OPT_STREAM_MIN_ITEMS must be >= 0");
       x->stream_min_items = value;
+      return BB_OK;
+    case BB_OPT_STREAM_REFINE:
+      if (value < -1 || value > 1) return fail(BB_E_ARG, "BB_OPT_STREAM_REFINE must be -1, 0 or 1");
+      x->refine_opt = (int)value;
       return BB_OK;
     case BB_OPT_WORKSPACE_BYTES:
       if (value < (1ll << 20)) return fail(BB_E_ARG, "BB_OPT_WORKSPACE_BYTES must be >= 1 MiB");

@@ -150,6 +150,8 @@ struct CandSelectArgs {
   int32_t* out_counts;
   int32_t k_final;
   uint32_t* overflow;        // set to 1 when a region overflowed (results of that row invalid)
+  const uint64_t* carry_in;  // [B][K] exact list of an earlier item range (joins the candidates), or null
+  const uint64_t* max_in;    // [B] rank-0 key of that range (with cand_pmax), or null
 };
 
 struct FinalizeArgs {

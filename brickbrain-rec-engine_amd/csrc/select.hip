@@ -649,7 +649,7 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
 
   // region counts -> exclusive prefix (each thread owns up to 4 consecutive regions)
   uint32_t c[4], sum = 0, ovf = 0;
-  uint64_t gm = 0;
+  uint64_t gm = (a.cand_pmax && a.max_in && tid == 0) ? a.max_in[row] : 0ull;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int r = 4 * tid + j;
@@ -685,8 +685,10 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
     for (int i = 0; i < kSelectThreads / 64; ++i) gmax = red[i] > gmax ? red[i] : gmax;
     if (a.max_out && tid == 0) a.max_out[row] = gmax;
   }
-  // candidate i -> region by binary search over the prefix
+  // candidate i -> region by binary search over the prefix; i >= total: the carried list
+  const uint64_t* carry = a.carry_in ? a.carry_in + (size_t)row * a.K : nullptr;
   auto global_key = [&](int i) -> uint64_t {
+    if (i >= (int)total) return carry[i - (int)total];
     int lo = 0, hi = R;  // pre[lo] <= i < pre[hi]
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -695,7 +697,7 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
     }
     return a.cand[(rbase + lo) * (size_t)a.cap + (i - pre[lo])];
   };
-  const int n = (int)total;
+  const int n = (int)total + (carry ? a.K : 0);
   const uint64_t* src = nullptr;
   if (n <= kCandCap) {
     for (int i = tid; i < n; i += kSelectThreads) cand[i] = global_key(i);

@@ -190,10 +190,14 @@ int bb_get_profile(bb_index* idx, bb_profile* out);
  *                           slab); auto = when the index has >= BB_OPT_STREAM_MIN_ITEMS rows.
  *                           Results are identical either way.
  *   BB_OPT_STREAM_MIN_ITEMS rows from which auto streams (default 100000)
- *   BB_OPT_WORKSPACE_BYTES  score-slab workspace cap (default 512 MiB) */
+ *   BB_OPT_WORKSPACE_BYTES  score-slab workspace cap (default 512 MiB; streaming may use up
+ *                           to 4 GiB unless this is set)
+ *   BB_OPT_STREAM_REFINE    -1 auto (default), 0 never, 1 always (index >= 2x the pilot): the
+ *                           two-level streaming bound.  Results are identical either way. */
 #define BB_OPT_STREAM 1
 #define BB_OPT_STREAM_MIN_ITEMS 2
 #define BB_OPT_WORKSPACE_BYTES 3
+#define BB_OPT_STREAM_REFINE 4
 int bb_set_option(bb_index* idx, int32_t option, int64_t value);
 
 /* Stored (normalised, index-dtype) item rows of B global ids into out (B×d, row-major;

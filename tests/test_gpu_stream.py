@@ -24,16 +24,18 @@ def brickrec():
 
 
 def _both(idx, mode, k, stream_gemms=None, **kw):
-    """(stream results, slab results) of one search.  stream_gemms: the scan launches the
-    streaming search must take (pilot + stream pass per side and query chunk) — more means a
-    candidate region overflowed and the search silently reran on the slab path."""
+    """(stream results, slab results) of one search.  The streaming search must finish on
+    the streaming path: no overflow handed back to the slab path (profile "rerun"), and at
+    least stream_gemms scan launches (pilot + streaming passes per side and query chunk;
+    the two-level bound adds a pass on indexes >= 4x the pilot)."""
     idx.set_option("stream", 1)
     idx.set_profiling(True)
     a = idx.search(mode, k, **kw)
     prof = idx.profile()
     idx.set_profiling(False)
+    assert prof["rerun"]["launches"] == 0, prof
     if stream_gemms is not None:
-        assert prof["gemm"]["launches"] == stream_gemms, prof
+        assert prof["gemm"]["launches"] >= stream_gemms, prof
     idx.set_option("stream", 0)
     b = idx.search(mode, k, **kw)
     idx.set_option("stream", -1)
@@ -192,3 +194,40 @@ def test_stream_large_bf16_torch_upload(brickrec):
     for i in range(32):
         if (rs[i, k - 1] - rs[i, k]).item() > 1e-5:
             assert set(ids[i].tolist()) == set(ri[i, :k].tolist())
+
+
+@pytest.mark.parametrize("dtype,mode", [("bf16", "similar"), ("f32", "semantic")])
+def test_stream_two_level_bound(brickrec, dtype, mode):
+    """Two-level streaming bound: a workspace too small for a 1/16 pilot leaves the pilot
+    at 8192 rows of 200,000 (n >= 16·n0), so the stream runs pass A over [0, n1), an exact
+    candidate select of that range whose last key bounds pass B over [n1, n), and a final
+    select over pass B's candidates plus pass A's list (rank 0 carried across).  Three scan
+    launches, no slab rerun, and the lists equal the slab path's exactly."""
+    n, d, B, k = 200000, 384, 256, 50
+    x = R.unit_rows(n, d, 61)
+    rng = np.random.default_rng(62)
+    mask = rng.random(n) < 0.6
+    idx = brickrec.ItemIndex(dtype=dtype)
+    idx.upload_items(x)
+    idx.set_option("workspace_bytes", 8 << 20)
+    idx.set_option("stream_refine", 1)   # auto takes it from 500K rows
+    if mode == "similar":
+        qi = rng.choice(n, B, replace=False)
+        kw = dict(q_items=qi, mask=mask)
+    else:
+        kw = dict(q_rows=R.unit_rows(B, d, 63), mask=mask)
+    idx.set_option("stream", 1)
+    idx.set_profiling(True)
+    a = idx.search(mode, k, **kw)
+    prof = idx.profile()
+    idx.set_profiling(False)
+    assert prof["rerun"]["launches"] == 0, prof
+    assert prof["gemm"]["launches"] == 3, prof
+    assert prof["select"]["launches"] == 3, prof   # pilot slab, pass A list, final
+    idx.set_option("stream", 0)
+    b = idx.search(mode, k, **kw)
+    _same(a, b)
+    assert np.all(a[2] == k)
+    if mode == "similar":
+        for i in range(B):
+            assert qi[i] not in set(a[1][i]) and mask[a[1][i]].all()
