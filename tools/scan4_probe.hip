@@ -110,6 +110,8 @@ int main() {
             {"s2_full", l2<96, 0>, 0}, {"s2_no_epi", l2<96, 1>, 0}, {"s2_mfma_lds_only", l2<96, 7>, 0}};
     else
       vs = {{"s4_full", l4<48, 0>, 0}, {"s4_no_stores", l4<48, 24>, 0}, {"s4_no_epi", l4<48, 1>, 0},
+            {"s4_chains_full", l4<48, 1024>, 0}, {"s4_chains_no_stores", l4<48, 24 | 1024>, 0},
+            {"s4_chains_mfma_lds_only", l4<48, 7 | 1024>, 0},
             {"s4_no_staging", l4<48, 2 | 24>, 0}, {"s4_mfma_lds_only", l4<48, 7>, 0},
             {"s4_no_stores_c32", l4<48, 24>, 32}, {"s4_no_stores_c64", l4<48, 24>, 64},
             {"s2_full", l2<48, 0>, 0}, {"s2_no_epi", l2<48, 1>, 0}, {"s2_mfma_lds_only", l2<48, 7>, 0}};
