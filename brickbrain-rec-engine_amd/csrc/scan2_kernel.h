@@ -1,7 +1,7 @@
 // scan2_kernel.h — query-resident MFMA scan with the epilogue woven into the MFMA stream.
 //
 // Same contract and data flow as scan_kernel.h (queries resident in VGPRs, 32-item tiles
-// staged by LDS-DMA into an XOR-swizzled double buffer, S + per-tile maxima epilogue),
+// staged by LDS-DMA into an XOR-swizzled three-deep ring, S + per-tile maxima epilogue),
 // restructured for the single wave per SIMD that this register budget allows:
 //   * tiles alternate between two accumulator sets (even / odd), so tile t-1's epilogue
 //     (accumulator reads, order images, S stores, tile maxima) and tile t+1's staging are
@@ -209,7 +209,11 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   constexpr int PIECES = KU / 8;          // 1 KiB LDS-DMA pieces per wave per tile
   static_assert(ROWB <= kScanRowMax, "row too wide for the scan kernel");
   static_assert(KU % 8 == 0, "KU must split into whole 1 KiB pieces per wave");
-  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_B];
+  // three-deep tile ring: two tiles of LDS-DMA in flight behind the one being read.  Small
+  // batches (B <= 128: one query group, 256 item chunks) are HBM-latency bound — one tile in
+  // flight per CU delivered ~4.3 TB/s on a 10M-row index.
+  constexpr int kRing = 3;
+  __shared__ __attribute__((aligned(16))) char smem[kRing * TILE_B];
 
   const int n_groups = a.Mpad / (kScanWaves * 32);
   const int total = n_groups * n_chunks;
@@ -287,6 +291,11 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   // first tile
 #pragma unroll
   for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
+  {
+    const int t1 = tile_lo + 1 < tile_hi ? tile_lo + 1 : tile_lo;
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) stage_piece(t1, 1, p);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   asm volatile("s_nop 4");
@@ -301,11 +310,11 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   // NOT overlap (it holds the SIMD's vector issue), so the epilogue is kept to ~25 VALU in
   // the common all-eligible case (tile_maxima fast path).
   constexpr int kEpiSlices = 8 + PIECES;
-  auto tile_body = [&](auto BUF, auto EPI, int tile, f32x16s& c, const f32x16s& p) __attribute__((always_inline)) {
-    constexpr int buf = decltype(BUF)::value;
+  auto tile_body = [&](int buf, auto EPI, int tile, f32x16s& c, const f32x16s& p) __attribute__((always_inline)) {
+    const int sbuf = buf == 0 ? 2 : buf - 1;  // (buf + 2) % kRing: the buffer tile-1 used
     constexpr bool epi = decltype(EPI)::value && !(ABL & 1);
     const int ptile = tile - 1;
-    const int stile = tile + 1 < tile_hi ? tile + 1 : tile;  // branch-free staging target
+    const int stile = tile + 2 < tile_hi ? tile + 2 : tile_hi - 1;  // branch-free staging target
     uint32_t te = 0, tp = 0;
     const int ptile0 = ptile * 32;
     // item fragments: ds_read issued two u-steps ahead of their MFMAs
@@ -370,11 +379,14 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
               (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
             }
           } else if constexpr (s == 7) {
-            nw_p = a.present[w0 + tile];
-            nw_m = a.mask[w0 + tile];
-            nw_e = erow[w0 + tile];
+            // as inline asm: a compiler-visible load would get a compiler wait before its
+            // first use that also waits for the (asm, invisible) DMA of tile + 2; these
+            // complete under the explicit end-of-tile wait (they are older than the DMA)
+            asm volatile("global_load_dword %0, %1, off" : "=v"(nw_p) : "v"(a.present + w0 + tile) : "memory");
+            asm volatile("global_load_dword %0, %1, off" : "=v"(nw_m) : "v"(a.mask + w0 + tile) : "memory");
+            asm volatile("global_load_dword %0, %1, off" : "=v"(nw_e) : "v"(erow + w0 + tile) : "memory");
           } else {
-            if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s - 8);
+            if constexpr (!(ABL & 2)) stage_piece(stile, sbuf, s - 8);
           }
         }
       });
@@ -383,13 +395,22 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     // ties the accumulator to a wait long enough for the last MFMA to retire, before any
     // register copy or read of it the compiler may place after this point.
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" : "+v"(c));
+    if constexpr (!(ABL & 4)) {
+      // the last PIECES vector-memory ops are tile + 2's DMA (the staging slices come
+      // last, asm "memory" clobbers keep that order): leave them in flight
+      if constexpr (ABL & 2)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+      __syncthreads();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (probe) the asm word loads
+    }
+    // the words are complete here; the tie keeps every use of them after the wait
+    asm volatile("" : "+v"(nw_p), "+v"(nw_m), "+v"(nw_e));
     pw = nw_p;
     mw = nw_m;
     ew = nw_e;
-    if constexpr (!(ABL & 4)) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
   };
 
   // final epilogue of the last tile (not overlapped)
@@ -412,25 +433,25 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
   };
 
-  using B0 = std::integral_constant<int, 0>;
-  using B1 = std::integral_constant<int, 1>;
   using EY = std::integral_constant<bool, true>;
   using EN = std::integral_constant<bool, false>;
-  tile_body(B0{}, EN{}, tile_lo, accE, accO);
-  int tile = tile_lo + 1;
+  tile_body(0, EN{}, tile_lo, accE, accO);
+  int tile = tile_lo + 1, buf = 1;  // tile t reads buffer (t - tile_lo) % kRing
   for (;;) {
     if (tile >= tile_hi) {
       last_epilogue(tile - 1, accE);
       break;
     }
-    tile_body(B1{}, EY{}, tile, accO, accE);
+    tile_body(buf, EY{}, tile, accO, accE);
     ++tile;
+    buf = buf == kRing - 1 ? 0 : buf + 1;
     if (tile >= tile_hi) {
       last_epilogue(tile - 1, accO);
       break;
     }
-    tile_body(B0{}, EY{}, tile, accE, accO);
+    tile_body(buf, EY{}, tile, accE, accO);
     ++tile;
+    buf = buf == kRing - 1 ? 0 : buf + 1;
   }
   if constexpr (STREAM) stream_end(a, region, sl);
 }
