@@ -700,7 +700,24 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
   const int n = (int)total + (carry ? a.K : 0);
   const uint64_t* src = nullptr;
   if (n <= kCandCap) {
-    for (int i = tid; i < n; i += kSelectThreads) cand[i] = global_key(i);
+    // gather by region (each region's keys are contiguous): a group of threads per region,
+    // four independent loads in flight per thread — no per-key binary search and no chain
+    // of dependent global loads
+    const int tpr = R >= kSelectThreads ? 1 : kSelectThreads / R;
+    for (int r = tid / tpr; r < R; r += kSelectThreads / tpr) {
+      const int base = (int)pre[r], cnt = (int)pre[r + 1] - base;
+      const uint64_t* sp = a.cand + (rbase + r) * (size_t)a.cap;
+      int i = tid % tpr;
+      for (; i + 3 * tpr < cnt; i += 4 * tpr) {
+        const uint64_t k0 = sp[i], k1 = sp[i + tpr], k2 = sp[i + 2 * tpr], k3 = sp[i + 3 * tpr];
+        cand[base + i] = k0;
+        cand[base + i + tpr] = k1;
+        cand[base + i + 2 * tpr] = k2;
+        cand[base + i + 3 * tpr] = k3;
+      }
+      for (; i < cnt; i += tpr) cand[base + i] = sp[i];
+    }
+    for (int i = (int)total + tid; i < n; i += kSelectThreads) cand[i] = carry[i - (int)total];
     __syncthreads();
     src = cand;
   }
@@ -717,6 +734,36 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
     if (n <= 64) wave_sort_emit<1>(src, n, sa, row, drop);
     else if (n <= 128) wave_sort_emit<2>(src, n, sa, row, drop);
     else wave_sort_emit<4>(src, n, sa, row, drop);
+    return;
+  }
+  if (src && n <= 4 * 512 && a.K <= 128) {
+    // up to 2048 candidates in LDS and K <= 128 (every configs[3]/[4] search): each wave
+    // sorts its 512-key quarter in registers (no barriers) and writes its top K, packed;
+    // wave 0 sorts the <= 4·K survivors and emits.  Replaces the 6-pass radix select
+    // (4096-bin histograms and a barrier per phase) for the common case.
+    const int nw = min(max(n - wave * 512, 0), 512);
+    int off = 0;
+    for (int w = 0; w < wave; ++w) off += min(min(max(n - w * 512, 0), 512), a.K);
+    uint64_t v[8];
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {
+      const int e = s8 * 64 + lane;
+      v[s8] = e < nw ? src[wave * 512 + e] : 0ull;
+    }
+    wave_bitonic_desc<8>(v, lane);
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {
+      const int e = s8 * 64 + lane;
+      if (e < min(nw, a.K)) sel[off + e] = v[s8];
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    int m = 0;
+    for (int w = 0; w < kSelectThreads / 64; ++w) m += min(min(max(n - w * 512, 0), 512), a.K);
+    if (m <= 64) wave_sort_emit<1>(sel, m, sa, row, drop);
+    else if (m <= 128) wave_sort_emit<2>(sel, m, sa, row, drop);
+    else if (m <= 256) wave_sort_emit<4>(sel, m, sa, row, drop);
+    else wave_sort_emit<8>(sel, m, sa, row, drop);
     return;
   }
   // more than 256: the K-th largest key, then the keys >= it (exactly min(K, n) of them)
