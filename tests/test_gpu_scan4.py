@@ -134,3 +134,46 @@ def test_scan4_stream_equals_slab(brickrec):
     sel = np.arange(0, B, 37)
     sim = xs[qi[sel]] @ xs.T
     _check(a[0][sel], a[1][sel], sim, k, allowed=lambda i: mask, drop=qi[sel])
+
+
+def test_scan4_hybrid_bf16_stream_and_slab(brickrec):
+    """bf16 hybrid (content similar-sets + CF with rated exclusions, under a mask), B = 300
+    -> both sides on scan4; streaming forced == slab, and both against the union blend of
+    the reference restatement over the device's bf16 operands (finalize1 path)."""
+    n, d, r, B, k = 120000, 384, 50, 300, 20
+    x = R.unit_rows(n, d, 71)
+    rng = np.random.default_rng(72)
+    f = rng.normal(0, 0.1, (n, r)).astype(np.float32)
+    u = rng.normal(0, 0.1, (B, r)).astype(np.float32)
+    mask = rng.random(n) < 0.5
+    rated = rng.random((B, n)) < 0.01
+    qi = rng.choice(n, B, replace=False)
+    idx = brickrec.ItemIndex(dtype="bf16")
+    idx.upload_items(x)
+    idx.upload_cf(f)
+    kw = dict(q_items=qi, q_cf=u, mask=mask, excl=rated)
+    idx.set_option("stream", 1)
+    idx.set_profiling(True)
+    a = idx.search("hybrid", k, **kw)
+    prof = idx.profile()
+    idx.set_profiling(False)
+    assert prof["rerun"]["launches"] == 0, prof
+    idx.set_option("stream", 0)
+    b = idx.search("hybrid", k, **kw)
+    for p_, q_ in zip(a, b):
+        assert np.array_equal(p_, q_)
+    xs, fs, us = _unit_bf16(x), _bf16(f), _bf16(u)
+    close = 0
+    for i in range(0, B, 23):
+        cs = xs[qi[i]] @ xs.T
+        ok = mask.copy()
+        ok[int(np.argmax(cs))] = False          # rank 0: the unmasked arg-max
+        c_i, c_s = R.topk_indices(cs, 2 * k, ok)
+        f_i, f_s = R.topk_indices(fs @ us[i], 2 * k, mask & ~rated[i])
+        ri, rsc = R.union_blend(c_i, c_s, f_i, f_s, 0.4, 0.6, k + 1)
+        np.testing.assert_allclose(a[0][i], rsc[:k], atol=TOL, rtol=0)
+        if len(rsc) <= k or rsc[k - 1] - rsc[k] > 2e-6:
+            assert set(a[1][i]) == set(ri[:k]), i
+        else:
+            close += 1
+    assert close <= 2
