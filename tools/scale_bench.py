@@ -59,7 +59,7 @@ def unit_rows(n, d, seed, dev, chunk=1 << 20):
     return out
 
 
-def run_case(name, c, seconds, dev, stream=-1):
+def run_case(name, c, seconds, dev, stream=-1, inflight=1):
     import torch
     import brickrec
     n, d, B, k, dt = c["n"], c["d"], c["B"], c["k"], c["dtype"]
@@ -67,6 +67,13 @@ def run_case(name, c, seconds, dev, stream=-1):
     idx = brickrec.ItemIndex(device=dev.index, dtype=dt)
     idx.upload_items(x, prenormalized=True)
     idx.set_option("stream", stream)
+    # extra lanes for the in-flight throughput (bench.py's scheme): own handle, stream, copy
+    lanes = []
+    for j in range(1, inflight):
+        lj = brickrec.ItemIndex(device=dev.index, dtype=dt)
+        lj.upload_items(x, prenormalized=True)
+        lj.set_option("stream", stream)
+        lanes.append(lj)
     del x
     torch.cuda.empty_cache()
     kw = {}
@@ -78,6 +85,8 @@ def run_case(name, c, seconds, dev, stream=-1):
         rng = np.random.default_rng(7)
         f = rng.normal(0, 0.1, (n, r)).astype(np.float32)
         idx.upload_cf(f)
+        for lj in lanes:
+            lj.upload_cf(f)
         mask = rng.random(n) < 0.10
         words = brickrec.engine.bits_from_bool(mask).view(np.int32)
         kw = dict(q_items=torch.from_numpy(rng.integers(0, n, B)).to(dev),
@@ -129,6 +138,25 @@ def run_case(name, c, seconds, dev, stream=-1):
            "frac_end_to_end": round(flops / (el / steps) / 1e12 / peak, 4),
            "alg_bytes": nbytes,
            "hbm_frac_end_to_end": round(nbytes / (el / steps) / 1e9 / HBM, 4)}
+    if lanes:
+        # `inflight` batches in flight on as many streams, steps alternating between them
+        runs = [(s, run)]
+        for lj in lanes:
+            sj = torch.cuda.Stream(dev)
+            runs.append((sj, lj.prepared_search(c["mode"], k, stream=sj, **kw)[0]))
+        for i in range(2 * len(runs)):
+            runs[i % len(runs)][1]()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            runs[i % len(runs)][1]()
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t0
+        out["inflight"] = inflight
+        out["qps_inflight"] = round(B * steps / el2, 1)
+        out["frac_end_to_end_inflight"] = round(flops / (el2 / steps) / 1e12 / peak, 4)
+        for lj in lanes:
+            lj.close()
     idx.close()
     torch.cuda.empty_cache()
     return out
@@ -140,13 +168,14 @@ def main():
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--stream", type=int, default=-1, help="-1 auto, 0 slab path, 1 streaming top-K")
+    ap.add_argument("--inflight", type=int, default=1, help="also measure with this many batches in flight")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     f = open(args.out, "a") if args.out else None
     for name in args.cases.split(","):
-        res = run_case(name, CASES[name], args.seconds, dev, args.stream)
+        res = run_case(name, CASES[name], args.seconds, dev, args.stream, args.inflight)
         line = json.dumps(res)
         print(line, flush=True)
         if f:
