@@ -10,14 +10,19 @@
 //
 // Registers (one wave per SIMD, 512 per lane): the two query blocks take 8·U registers
 // (U = 16-wide k steps; d = 768: 384, d = 384: 192).  The first 256 live in AGPRs, the rest
-// in VGPRs; both are legal MFMA B operands on gfx950.  There is ONE accumulator per block
-// (2 × 16 VGPRs), not the even/odd pair scan2 uses: the tile is two accumulation chains,
-// block A then block B, and each block's epilogue is woven into the OTHER block's chain:
-//   chain A of tile t  <- epilogue of block B of tile t-1, eligibility words of tile t+1,
-//                         LDS-DMA staging of tile t+1
-//   chain B of tile t  <- epilogue of block A of tile t
-// Item fragments are read from LDS once per chain (2 ds_read_b128 per 2 MFMAs, well inside
-// the LDS budget of one read per 32x32x16 gap).
+// in VGPRs; both are legal MFMA B operands on gfx950.  Two schedules:
+// * d <= 512 (interleaved, IL): per k-step one fragment read feeds A_u and B_u, two
+//   accumulator sets alternate with the tiles, and both blocks' epilogues of tile t-1 are
+//   woven into tile t after its DMA pieces.  Half the LDS fragment reads per MFMA: the
+//   MFMA + LDS loop runs at 1.52 PF/s against 1.34 for the chained schedule.
+// * d = 768 (chained): no registers for a second accumulator set, so ONE accumulator per
+//   block and the tile is two accumulation chains, block A then block B, each block's
+//   epilogue woven into the OTHER block's chain:
+//     chain A of tile t  <- epilogue of block B of tile t-1, eligibility words of tile t+1,
+//                           LDS-DMA staging of tile t+1
+//     chain B of tile t  <- epilogue of block A of tile t
+//   Item fragments are read once per chain (one ds_read_b128 per MFMA).
+// Measurements: tools/scan4_probe.hip, profiles/r01*_scan4_probe.jsonl.
 //
 // Same contract as scan2_kernel.h — LDS tile layout (XOR swizzle), XCD-aware blockIdx ->
 // (query group, item chunk) mapping, tile maxima for the slab select — except that scores
