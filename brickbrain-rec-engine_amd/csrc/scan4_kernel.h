@@ -117,8 +117,8 @@ __device__ __forceinline__ void s4_rank0(const GemmArgs& a, const f32x16s& p, in
 constexpr int scan4_at(int s, int U) { return (s + 2 < U) ? s + 2 : U - 1; }
 // chain A: block B's epilogue (slices 0..E-1 from u = 2, after the accumulator tie), the
 // next tile's words (slice E), then the LDS-DMA pieces spaced SP u-steps apart (slices
-// E+1..): each DMA holds the wave's issue for ~20+ cycles, and back to back they stalled
-// the MFMA stream (staging cost 14 % of the kernel with pieces on consecutive u-steps).
+// E+1..): each DMA holds the wave's issue for ~20+ cycles; spread out rather than back to
+// back they cost 2-3 % less (staging still costs ~14 % of the kernel: the DMA issue itself).
 constexpr int scan4_atA(int s, int U, int E, int pieces) {
   const int sp = (U - (E + 3)) / (pieces > 0 ? pieces : 1) > 1 ? (U - (E + 3)) / pieces : 1;
   const int u = s < E ? s + 2 : s == E ? E + 2 : E + 3 + (s - E - 1) * sp;
