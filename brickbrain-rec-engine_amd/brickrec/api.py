@@ -225,15 +225,32 @@ def create_app(dbcon, *, engine: Optional[Engine] = None, semantic=None, prepare
 
     @app.post("/sets/similar/semantic", response_model=List[NLSearchResult])
     def similar_semantic(query: SimilarSetQuery):
+        """The reference route's live behaviour (recommendation_api.py:1501-1585): the SQL
+        theme + piece-count heuristic, whatever index the app holds.  The reference runs it
+        on a fresh connection (:1513); here it runs under the app lock on the shared one."""
         try:
-            if semantic is not None:
-                return _similar_by_embedding(semantic, query)
-            return _similar_by_sql(dbcon, query)
+            with lock:
+                return _similar_by_sql(dbcon, query)
         except HTTPException:
             raise
         except Exception as e:
             logger.error(f"Semantic similarity search error: {e}")
             raise HTTPException(status_code=500, detail=f"Database error: {str(e)}")
+
+    @app.post("/sets/similar/embedding", response_model=List[NLSearchResult])
+    def similar_embedding(query: SimilarSetQuery):
+        """New route (no reference counterpart): embedding KNN of the stored set over the
+        loaded SemanticIndex — the branch the reference route never reaches (:1587-1759)."""
+        if semantic is None:
+            raise HTTPException(status_code=400, detail="no semantic index loaded")
+        try:
+            with lock:
+                return _similar_by_embedding(semantic, query)
+        except HTTPException:
+            raise
+        except Exception as e:
+            logger.error(f"Embedding similarity search error: {e}")
+            raise HTTPException(status_code=500, detail=str(e))
 
     @app.post("/recommendations/batch", response_model=BatchResult)
     def batch(q: BatchQuery):
@@ -295,7 +312,7 @@ def _similar_by_sql(dbcon, query: SimilarSetQuery) -> List[NLSearchResult]:
 
 
 def _similar_by_embedding(semantic, query: SimilarSetQuery) -> List[NLSearchResult]:
-    """Embedding KNN of the stored set (the route's intended, previously dead, branch)."""
+    """Embedding KNN of the stored set (served by the opt-in /sets/similar/embedding route)."""
     if query.set_num not in semantic.pos:
         raise HTTPException(status_code=404, detail="Set not found")
     sc, ids, cnt = semantic.similar_to([query.set_num], query.top_k)

@@ -24,6 +24,10 @@ row. The ranks therefore first assemble the query rows: each rank fetches the ro
 (``bb_get_rows``) and an all-reduce(sum) fills in the rest. Then every shard scans with
 the same ``q_rows``, which is ``feat_matrix[target]`` (recommendation_system.py:213).
 
+A rank whose block is empty (N < P·⌈N/P⌉ leaves the last ranks without rows, e.g. N=5 on
+4 ranks) uploads nothing and contributes empty key lists (key 0 = empty slot) to the
+gather; it still runs the merge, so every rank returns the same results.
+
 At 25K items the index does not shard (39 MB); ``bench.py --gpus N`` runs replicas.
 """
 from __future__ import annotations
@@ -65,6 +69,7 @@ class ShardedIndex:
         self.world = dist.get_world_size(group)
         self.n = int(n_items)
         self.lo, self.hi = shard_bounds(self.n, self.world, self.rank)
+        self.empty = self.hi <= self.lo
         if index_factory is not None:
             self.local = index_factory(self.lo)
         else:
@@ -80,13 +85,20 @@ class ShardedIndex:
 
     def upload_items(self, rows, prenormalized: bool = False, present=None):
         """rows: the full [N, d] matrix (each rank keeps its block) or this rank's block."""
+        self.d = int(rows.shape[1])
+        if self.empty:
+            return
         self.local.upload_items(self._mine(rows), prenormalized=prenormalized,
                                 present=None if present is None else self._mine(np.asarray(present)))
 
     def upload_cf(self, factors, present=None):
+        if self.empty:
+            return
         self.local.upload_cf(self._mine(factors), present=None if present is None else self._mine(np.asarray(present)))
 
     def upload_attrs(self, num_parts, year, theme_id):
+        if self.empty:
+            return
         self.local.upload_attrs(self._mine(np.asarray(num_parts)), self._mine(np.asarray(year)),
                                 self._mine(np.asarray(theme_id)))
 
@@ -96,10 +108,13 @@ class ShardedIndex:
         import torch
         import torch.distributed as dist
         ids = torch.as_tensor(item_ids, dtype=torch.int64)
-        mine = (ids >= self.lo) & (ids < self.hi)
-        rows = self.local.get_rows(ids.to(self._device()))
-        rows = torch.as_tensor(rows).to(self._device()).float()
-        rows[~mine.to(rows.device)] = 0
+        if self.empty:
+            rows = torch.zeros((int(ids.shape[0]), self.d), dtype=torch.float32, device=self._device())
+        else:
+            mine = (ids >= self.lo) & (ids < self.hi)
+            rows = self.local.get_rows(ids.to(self._device()))
+            rows = torch.as_tensor(rows).to(self._device()).float()
+            rows[~mine.to(rows.device)] = 0
         dist.all_reduce(rows, group=self.group)
         return rows
 
@@ -125,8 +140,14 @@ class ShardedIndex:
             loc_excl = torch.as_tensor(bits_from_bool(loc_excl.numpy()).view(np.int32)).to(dev)
         q_rows = None if q_rows is None else torch.as_tensor(q_rows).to(dev).float().contiguous()
         q_cf = None if q_cf is None else torch.as_tensor(q_cf).to(dev).float().contiguous()
-        keys, maxk = self.local.search_keys(mode, k, q_rows=q_rows, q_cf=q_cf, mask=loc_mask, excl=loc_excl,
-                                            k_side=k_side)
+        if self.empty:   # no rows here: empty lists (key 0) for the gather
+            sides, kint = self.local.key_lens(mode, k, k_side)
+            B = int((q_rows if q_rows is not None else q_cf).shape[0])
+            keys = torch.zeros((sides, B, kint), dtype=torch.int64, device=dev)
+            maxk = torch.zeros((B,), dtype=torch.int64, device=dev)
+        else:
+            keys, maxk = self.local.search_keys(mode, k, q_rows=q_rows, q_cf=q_cf, mask=loc_mask,
+                                                excl=loc_excl, k_side=k_side)
         all_keys = _all_gather(keys, self.group, self.world)   # [P, sides, B, k_int]
         all_max = _all_gather(maxk, self.group, self.world)    # [P, B]
         return self.local.finalize(mode, k, all_keys, all_max, self.world, k_side=k_side,

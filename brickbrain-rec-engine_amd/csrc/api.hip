@@ -83,6 +83,12 @@ struct bb_index {
   int refine_opt = -1;                 // BB_OPT_STREAM_REFINE
   hipStream_t stream = nullptr;
   std::mutex mu;
+  // Cross-stream ordering of the shared workspace: every call records `done` on the stream it
+  // ran on; a call arriving on a different stream first waits for that event, so two calls
+  // on two streams never overlap on the same scratch buffers.
+  hipEvent_t done = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool has_last = false;
 
   int64_t n = 0, Npad = 0;
   int d = 0, Dpad = 0;
@@ -123,6 +129,19 @@ struct DeviceGuard {
   }
 };
 
+// Order this call after the handle's previous call when that one ran on another stream.
+int enter_stream(bb_index* x, hipStream_t s) {
+  if (x->has_last && x->last_stream != s) BB_HIP(hipStreamWaitEvent(s, x->done, 0));
+  return BB_OK;
+}
+// Mark the end of this call's work on s (the next call on another stream waits for it).
+int leave_stream(bb_index* x, hipStream_t s) {
+  BB_HIP(hipEventRecord(x->done, s));
+  x->last_stream = s;
+  x->has_last = true;
+  return BB_OK;
+}
+
 // Run a launcher with optional event bracketing for the profiler.
 template <typename F>
 int timed(bb_index* x, int fam, hipStream_t s, F&& launch) {
@@ -161,6 +180,10 @@ int to_device(bb_index* x, DevBuf& buf, size_t off, const void* src, size_t byte
   BB_HIP(hipMemcpyAsync((char*)buf.p + off, src, bytes, hipMemcpyHostToDevice, s));
   *out = (char*)buf.p + off;
   return BB_OK;
+}
+
+hipStream_t call_stream(bb_index* x, const bb_query* q) {
+  return (q->flags & BB_Q_NULL_STREAM) ? (hipStream_t)0 : q->stream ? (hipStream_t)q->stream : x->stream;
 }
 
 int side_k_int(const bb_query* q, int32_t* sides, int32_t* k_int) {
@@ -217,6 +240,12 @@ int bb_create(const bb_desc* desc, bb_index** out) {
     delete x;
     return fail(BB_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
+  e = hipEventCreateWithFlags(&x->done, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    (void)hipStreamDestroy(x->stream);
+    delete x;
+    return fail(BB_E_HIP, std::string("hipEventCreate: ") + hipGetErrorString(e));
+  }
   *out = x;
   return BB_OK;
 }
@@ -235,6 +264,8 @@ int bb_destroy(bb_index* x) {
                       &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
+    if (x->has_last) (void)hipEventSynchronize(x->done);
+    (void)hipEventDestroy(x->done);
     (void)hipStreamDestroy(x->stream);
   }
   delete x;
@@ -258,6 +289,7 @@ int bb_get_rows(bb_index* x, const int64_t* ids, int32_t B, void* out, int32_t w
   const size_t es = elem_size(x->dtype);
   const int bpad = (int)round_up(B, kTileRows);
   int rc;
+  if ((rc = enter_stream(x, x->stream))) return rc;
   if ((rc = x->tmp.ensure((size_t)bpad * x->Dpad * es + (size_t)B * 8 + 256))) return rc;
   char* rows = (char*)x->tmp.p;
   const int64_t* d_ids = ids;
@@ -281,7 +313,7 @@ int bb_get_rows(bb_index* x, const int64_t* ids, int32_t B, void* out, int32_t w
   BB_HIP(hipMemcpy2DAsync(out, (size_t)x->d * es, rows, (size_t)x->Dpad * es, (size_t)x->d * es, B,
                           where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, x->stream));
   BB_HIP(hipStreamSynchronize(x->stream));
-  return BB_OK;
+  return leave_stream(x, x->stream);
 }
 
 // Upload rows (host or device) in chunks through the staging buffer and convert them into
@@ -330,6 +362,7 @@ int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t
   if (n >= 0xFFFFFFFFll - x->id_offset) return fail(BB_E_ARG, "too many items for 32-bit ids");
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
+  if (int rc0 = enter_stream(x, x->stream)) return rc0;
   x->n = n;
   x->d = d;
   x->Npad = round_up(n, kTileRows);
@@ -351,7 +384,8 @@ int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t
   BB_HIP(hipMemsetAsync(x->ones.p, 0xFF, wbytes, x->stream));
   BB_HIP(hipMemsetAsync(x->zeros.p, 0, wbytes, x->stream));
   if ((rc = upload_rows(x, rows, n, d, in_dtype, prenormalized ? 0 : 1, where, x->items.p, x->Dpad))) return rc;
-  return make_planes(x, x->items, x->items3, x->Dpad);
+  if ((rc = make_planes(x, x->items, x->items3, x->Dpad))) return rc;
+  return leave_stream(x, x->stream);
 }
 
 int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const uint32_t* present_bits) {
@@ -359,6 +393,7 @@ int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const 
   if (x->n <= 0) return fail(BB_E_STATE, "upload items before CF factors");
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
+  if (int rc0 = enter_stream(x, x->stream)) return rc0;
   x->r = r;
   x->Rpad = (int)round_up(r, gemm_tile_k(x->dtype));
   const size_t bytes = (size_t)x->Npad * x->Rpad * elem_size(x->dtype);
@@ -375,7 +410,8 @@ int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const 
     BB_HIP(hipMemsetAsync(x->cf_present.p, 0xFF, wbytes, x->stream));
   }
   if ((rc = upload_rows(x, f, x->n, r, in_dtype, 0, BB_HOST, x->cf.p, x->Rpad))) return rc;
-  return make_planes(x, x->cf, x->cf3, x->Rpad);
+  if ((rc = make_planes(x, x->cf, x->cf3, x->Rpad))) return rc;
+  return leave_stream(x, x->stream);
 }
 
 int bb_upload_attrs(bb_index* x, const int32_t* num_parts, const int16_t* year, const int32_t* theme_id) {
@@ -384,13 +420,14 @@ int bb_upload_attrs(bb_index* x, const int32_t* num_parts, const int16_t* year, 
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
   int rc;
+  if ((rc = enter_stream(x, x->stream))) return rc;
   if ((rc = x->parts.ensure(x->n * 4)) || (rc = x->year.ensure(x->n * 2)) || (rc = x->theme.ensure(x->n * 4)))
     return rc;
   BB_HIP(hipMemcpyAsync(x->parts.p, num_parts, x->n * 4, hipMemcpyHostToDevice, x->stream));
   BB_HIP(hipMemcpyAsync(x->year.p, year, x->n * 2, hipMemcpyHostToDevice, x->stream));
   BB_HIP(hipMemcpyAsync(x->theme.p, theme_id, x->n * 4, hipMemcpyHostToDevice, x->stream));
   BB_HIP(hipStreamSynchronize(x->stream));
-  return BB_OK;
+  return leave_stream(x, x->stream);
 }
 
 int bb_eval_mask(bb_index* x, const bb_predicate* p, uint32_t* out_bits, int32_t where) {
@@ -401,8 +438,9 @@ int bb_eval_mask(bb_index* x, const bb_predicate* p, uint32_t* out_bits, int32_t
   const int64_t nw = (x->n + 31) / 32;
   const size_t tb = (size_t)((std::max(p->n_theme_bits, 0) + 31) / 32) * 4;
   const size_t ib = (size_t)std::max<int64_t>(p->n_excluded, 0) * 8;
-  int rc = x->stage_in.ensure(nw * 4 + tb + ib + 64);
+  int rc = enter_stream(x, x->stream);
   if (rc) return rc;
+  if ((rc = x->stage_in.ensure(nw * 4 + tb + ib + 64))) return rc;
   char* base = (char*)x->stage_in.p;
   uint32_t* dout = where == BB_DEVICE ? out_bits : (uint32_t*)base;
   uint32_t* dtheme = (uint32_t*)(base + round_up(nw * 4, 16));
@@ -434,7 +472,7 @@ int bb_eval_mask(bb_index* x, const bb_predicate* p, uint32_t* out_bits, int32_t
     BB_HIP(hipMemcpyAsync(out_bits, dout, nw * 4, hipMemcpyDeviceToHost, x->stream));
   }
   BB_HIP(hipStreamSynchronize(x->stream));
-  return BB_OK;
+  return leave_stream(x, x->stream);
 }
 
 int bb_key_lens(const bb_query* q, int32_t* sides, int32_t* k_int) { return side_k_int(q, sides, k_int); }
@@ -464,7 +502,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   if (out_keys && (!res->keys || !res->max_keys)) return fail(BB_E_ARG, "BB_Q_OUT_KEYS needs keys/max_keys");
   if (!out_keys && (!res->scores || !res->ids)) return fail(BB_E_ARG, "null result buffers");
 
-  hipStream_t s = (q->flags & BB_Q_NULL_STREAM) ? (hipStream_t)0 : q->stream ? (hipStream_t)q->stream : x->stream;
+  const hipStream_t s = call_stream(x, q);
   const int where = q->where;
   const int64_t nw = (x->n + 31) / 32;
 
@@ -881,12 +919,17 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   if (!x || !q || !res) return fail(BB_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
-  int rc = search_locked(x, q, res, true);
+  const hipStream_t s = call_stream(x, q);
+  int rc = enter_stream(x, s);
+  if (rc) return rc;
+  rc = search_locked(x, q, res, true);
   if (rc == kRetrySlab) {
     if (x->prof) ++x->launches[K_RERUN];
     rc = search_locked(x, q, res, false);
   }
-  return rc;
+  // an error may leave work enqueued on s: the next call still orders after it
+  const int rc2 = leave_stream(x, s);
+  return rc ? rc : rc2;
 }
 
 int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint64_t* max_keys, int32_t n_parts,
@@ -898,7 +941,8 @@ int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint
   if (n_parts * K_int > 4096) return fail(BB_E_ARG, "bb_finalize: n_parts * k_int > 4096");
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
-  hipStream_t s = (q->flags & BB_Q_NULL_STREAM) ? (hipStream_t)0 : q->stream ? (hipStream_t)q->stream : x->stream;
+  const hipStream_t s = call_stream(x, q);
+  if ((rc = enter_stream(x, s))) return rc;
   const int B = q->B;
   const bool host_out = res->where != BB_DEVICE;
   if (host_out) {
@@ -931,7 +975,7 @@ int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint
     if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, x->out_cnt.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
     BB_HIP(hipStreamSynchronize(s));
   }
-  return BB_OK;
+  return leave_stream(x, s);
 }
 
 int bb_set_option(bb_index* x, int32_t option, int64_t value) {

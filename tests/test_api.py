@@ -111,6 +111,52 @@ def test_similar_semantic_sql_route(client):
     assert client.post("/sets/similar/semantic", json={"set_num": "nope-1"}).status_code == 404
 
 
+def test_similar_semantic_sql_pinned(client, golden):
+    """a14 pinned on the golden catalogue, computed here independently of brickrec.api: the
+    reference route (recommendation_api.py:1531-1558) returns sets of the target's theme with
+    num_parts in [max(1, int(0.5 p)), int(1.5 p)], num_parts > 0, the target excluded,
+    ordered by |Δparts| asc then year desc, LIMIT top_k, relevance max(0.1, 1 − Δ/max(p, p')).
+    Rows tied on (Δ, year) have no SQL order, so the comparison is per (Δ, year) group."""
+    g1 = golden("g1_content.npz")
+    cat = catalog_json()
+    rows = cat["row_set_nums"]
+    parts, year, theme = g1["num_parts"].astype(np.int64), g1["year"].astype(np.int64), g1["theme_id"]
+    checked = 0
+    for t in range(0, len(rows), 97):
+        p = int(parts[t])
+        lo, hi = max(1, int(p * 0.5)), int(p * 1.5)
+        cand = np.flatnonzero((theme == theme[t]) & (parts > 0) & (parts >= lo) & (parts <= hi)
+                              & (np.arange(len(rows)) != t))
+        diff = np.abs(parts[cand] - p)
+        order = np.lexsort((-year[cand], diff))
+        top_k = 10
+        exp = cand[order][:top_k]
+        r = client.post("/sets/similar/semantic", json={"set_num": rows[t], "top_k": top_k})
+        assert r.status_code == 200, r.text
+        res = r.json()
+        assert len(res) == len(exp)
+        got_keys = [(abs(x["num_parts"] - p), -x["year"]) for x in res]
+        assert got_keys == [(int(abs(parts[i] - p)), -int(year[i])) for i in exp]
+        for x in res:
+            i = rows.index(x["set_num"])
+            assert theme[i] == theme[t] and lo <= parts[i] <= hi and i != t
+            rel = max(0.1, 1.0 - abs(int(parts[i]) - p) / max(p, int(parts[i])))
+            assert x["relevance_score"] == pytest.approx(rel, abs=1e-12)
+            assert x["match_reasons"][:2] == [f"Same theme: {cat['theme_names'][i]}",
+                                              f"Similar size: {int(parts[i])} vs {p} pieces"]
+        # tie groups of (Δ, year) hold the same sets in any order
+        for key in set(got_keys):
+            assert ({x["set_num"] for x, kk in zip(res, got_keys) if kk == key} <=
+                    {rows[i] for i in cand if (int(abs(parts[i] - p)), -int(year[i])) == key})
+        checked += len(res) > 0
+    assert checked >= 5
+
+
+def test_embedding_route_is_opt_in(client):
+    """The embedding KNN is a separate route; without a SemanticIndex it refuses."""
+    assert client.post("/sets/similar/embedding", json={"set_num": "x"}).status_code == 400
+
+
 def test_errors(client):
     assert client.post("/recommendations", json={"recommendation_type": "content"}).status_code == 400
     assert client.post("/recommendations", json={"set_num": "x", "top_k": 0}).status_code == 422

@@ -337,3 +337,27 @@ def test_inflight_lanes_device(brickrec):
             np.testing.assert_allclose(sc[i], rs[:k], atol=TOL, rtol=0)
             if rs[k - 1] - rs[k] > 2e-6:
                 assert set(ids[i]) == set(ri[:k])
+
+
+def test_one_handle_two_streams(brickrec):
+    """One ItemIndex driven from two torch streams back to back, nothing synchronised in
+    between: the handle's scratch workspace is shared, so each call must order itself after
+    the previous call on the other stream (bb_index `done` event).  Every result equals the
+    same search run alone."""
+    import torch
+    n, d, B, k = 25216, 384, 256, 50
+    dev = torch.device("cuda", 0)
+    x = R.unit_rows(n, d, 1234)
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(torch.from_numpy(x).to(dev))
+    qs = [torch.from_numpy(R.unit_rows(B, d, 900 + j)).to(dev) for j in range(2)]
+    ref = [idx.search("semantic", k, q_rows=q.cpu().numpy()) for q in qs]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    outs = []
+    for it in range(12):
+        j = it & 1
+        outs.append((j, idx.search("semantic", k, q_rows=qs[j], stream=streams[j])))
+    torch.cuda.synchronize()
+    for j, (sc, ids, cnt) in outs:
+        assert np.array_equal(ids.cpu().numpy(), ref[j][1])
+        assert np.array_equal(sc.cpu().numpy(), ref[j][0])
