@@ -1,23 +1,31 @@
 """bench.py — similarity queries/sec + p50 latency on MI355X (BASELINE.json `metric`).
 
-Workload (configs[1]): batch of 256 query embeddings × 25,216 × 384-d item matrix, exact
-cosine top-50, one MI355X per rank.  A step = one bb_search over one batch with the item
-matrix and the queries already resident in HBM (MFMA scan with fused query normalisation
--> top-K select writing the final lists).  --inflight L (default 3) keeps L batches in
-flight per GPU: L index handles on L HIP streams, steps alternating between them, so one
-batch's latency-bound select and the scan's last-tile imbalance overlap the next batch's
-scan; every step still runs its complete search.  p50_ms is the per-step latency in that
-regime, p50_ms_serial the latency of one batch alone.  At 25K items the index does not
-shard: with --gpus N every rank serves its own batches against a full
-replica ("replicas only", weak scaling, no collective on the data path); value = queries
-of all ranks / max-over-ranks wall time.
+Workload (configs[1], the default line): batch of 256 query embeddings × 25,216 × 384-d item
+matrix, exact cosine top-50, one MI355X per rank.  A step = one bb_search over one batch
+with the item matrix and the queries already resident in HBM.  --inflight L (default 3)
+keeps L batches in flight per GPU: L index handles on L HIP streams, steps alternating
+between them, so one batch's latency-bound select overlaps the next batch's scan; every
+step still runs its complete search.  p50_ms is the per-step latency in that regime,
+p50_ms_serial the latency of one batch alone.  At 25K items the index does not shard
+(SURVEY.md §8e): with --gpus N every rank serves its own batches against a full replica
+("replicas only", weak scaling, no collective on the data path); value = queries of all
+ranks / max-over-ranks wall time.
 
---workload c4 / c5 runs the large-index configs instead (BASELINE.json configs[3] / [4]):
-1M x 768 bf16, B=4096, top-100 / 10M x 384 bf16, B=8192, top-100, the item rows sharded
-across the ranks (ShardedIndex: local streaming top-K, one RCCL all-gather of the candidate
-keys, bb_finalize merge).  Total items are fixed, so more GPUs means smaller shards
-("scaling": "strong"); value = queries answered per second by the whole job.  These are
-not the default line (configs[1] is, per BASELINE.json's metric) and run only on request.
+Other workloads (run on request, not the default line):
+  --workload c3   configs[2]: hybrid (liked-set content + CF r=50) + the constraint mask
+                  (num_parts <= 800 AND year >= 2015) + rated exclusions, B=1024, top-50, f32
+  --workload c4   configs[3]: 1M x 768 bf16, B=4096, top-100, rows sharded over the ranks
+  --workload c5   configs[4]: 10M x 384 bf16, B=8192, top-100, rows sharded over the ranks
+The sharded workloads (ShardedIndex: local streaming top-K, one RCCL all-gather of the
+candidate keys, bb_finalize merge) fix the total items, so more GPUs means smaller shards
+("scaling": "strong").
+
+Roofline (dominant kernel, HIP events on the library's launch stream): `achieved` is the
+MFMA work the scan kernel actually issues per second — algorithmic flops (2·B·N·d, SURVEY.md
+§8d) × the MFMA flops it executes per algorithmic flop (six bf16 products per fp32 product
+in the split-precision scan3, one for a bf16 index) — against the dense peak of that
+instruction (bf16 2.5 PF).  `f32_equivalent` prices the algorithmic flops against the f32
+MFMA peak (157.3 TF), which the split scan can exceed because it does not run on it.
 
 Launch: python bench.py [--gpus 1 --steps 500 --warmup 50]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -41,83 +49,124 @@ BF16_DENSE_TF = 2500.0   # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md), no
 F32_DENSE_TF = 157.3
 
 
-def scan_kernel_info(dtype):
-    """(kernel, MFMA instruction peak, MFMA flops executed per algorithmic flop).
-    An f32 index runs the split-precision scan: six bf16 MFMAs per fp32 product
-    (scan3_kernel.h, bf16x6, fp32-class accuracy) unless BB_NO_SPLIT forces the fp32 MFMA.
-    The roofline is priced on ALGORITHMIC flops (2·B·N·d) against the dense MFMA peak of the
-    arithmetic type the path computes in (f32: 157.3 TF, bf16: 2.5 PF); the bf16 MFMA issue
-    utilisation of the split kernel is reported beside it."""
+def scan_kernel_info(dtype, width):
+    """(kernel, MFMA flops executed per algorithmic flop) of the scan that runs for an index
+    of this dtype and padded width.  An f32 index runs the split-precision scan3 (six bf16
+    MFMA products per fp32 product, fp32-class accuracy) unless BB_NO_SPLIT forces the fp32
+    MFMA; a bf16 index runs scan2 / scan4 on the bf16 MFMA."""
     if os.environ.get("BB_FORCE_TILED_GEMM"):
         return "gemm_nt_kernel", 1.0
     if dtype == "f32" and not os.environ.get("BB_NO_SPLIT"):
-        return "scan3_kernel<48> (bf16x6 split, f32 accumulate)", 6.0
+        return f"scan3_kernel<{width * 2 // 16}> (bf16x6 split, f32 accumulate)", 6.0
     if dtype == "f32":
-        return "scan2_kernel<float,96> (fp32 MFMA)", 1.0
-    return "scan2_kernel<uint16_t,48> (bf16 MFMA)", 1.0
+        return "scan2_kernel<float> (fp32 MFMA)", 1.0
+    return "scan2/scan4_kernel<uint16_t> (bf16 MFMA)", 1.0
 
 
-def unit_rows_torch(n, d, seed, device):
+def roofline(flops_alg, bytes_alg, kernel_us, dtype, kname, mfma_per_flop, traffic):
+    """Roofline object of the dominant kernel: issued MFMA rate vs the issued instruction's
+    dense peak, plus the f32-equivalent pricing of the algorithmic flops."""
+    alg_tf = flops_alg / (kernel_us * 1e-6) / 1e12
+    issued = alg_tf * mfma_per_flop
+    peak = BF16_DENSE_TF if (dtype == "bf16" or mfma_per_flop > 1) else F32_DENSE_TF
+    out = {"bound": "mfma", "achieved": round(issued, 2), "peak": peak, "unit": "TFLOP/s",
+           "frac": round(issued / peak, 4), "traffic": traffic, "kernel": kname,
+           "kernel_us": round(kernel_us, 3),
+           "achieved_is": "issued MFMA TFLOP/s = algorithmic flops x mfma_flops_per_algorithmic_flop / kernel time",
+           "mfma_flops_per_algorithmic_flop": mfma_per_flop,
+           "algorithmic_tflops": round(alg_tf, 2),
+           "algorithmic_flops_per_launch": flops_alg, "algorithmic_bytes_per_launch": bytes_alg,
+           "hbm_frac_at_alg_bytes": round(bytes_alg / (kernel_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+    if dtype == "f32":
+        out["f32_equivalent"] = {"achieved": round(alg_tf, 2), "peak": F32_DENSE_TF,
+                                 "frac": round(alg_tf / F32_DENSE_TF, 4)}
+    return out
+
+
+def unit_rows_torch(n, d, seed, device, chunk=1 << 20):
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed)
-    x = torch.randn((n, d), generator=g, device=device, dtype=torch.float32)
-    return x / x.norm(dim=1, keepdim=True)
+    out = torch.empty((n, d), dtype=torch.float32, device=device)
+    for i in range(0, n, chunk):
+        x = torch.randn((min(chunk, n - i), d), generator=g, device=device, dtype=torch.float32)
+        out[i:i + x.shape[0]] = x / x.norm(dim=1, keepdim=True)
+    return out
 
 
-def load_pmc(dtype):
+def load_pmc(key):
     """HBM bytes per dominant-kernel launch from the committed rocprofv3 PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        e = d.get(dtype, {}).get("gemm")
+        e = d.get(key, {}).get("gemm")
         return None if e is None else float(e["hbm_bytes_per_launch"])
     except Exception:
         return None
 
 
-def cpu_baseline(x_np, q_np, k, budget_s=10.0, max_batches=400):
-    """The oracle's batched exact cosine top-k (numpy/BLAS) on the host cores."""
-    from oracle.restatement import batched_cosine_topk
+def _blas_threads():
     try:
         from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+        return max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
     except Exception:
-        cores = os.cpu_count() or 1
-    batched_cosine_topk(x_np, q_np[:8], k)  # warm BLAS
-    t0 = time.perf_counter()
-    nb = 0
+        return os.cpu_count() or 1
+
+
+def _time_cpu(fn, budget_s, max_calls):
+    fn()  # warm
     lat = []
-    ids0 = None
-    while nb < max_batches and time.perf_counter() - t0 < budget_s:
+    t0 = time.perf_counter()
+    while len(lat) < max_calls and time.perf_counter() - t0 < budget_s:
         t1 = time.perf_counter()
-        ids, sc = batched_cosine_topk(x_np, q_np, k)
+        fn()
         lat.append(time.perf_counter() - t1)
-        if ids0 is None:
-            ids0 = ids
-        nb += 1
-    el = time.perf_counter() - t0
-    out = {"value": round(nb * q_np.shape[0] / el, 1), "unit": "queries/s", "cores": int(cores),
-           "kind": "port", "p50_ms": round(1e3 * float(np.median(lat)), 3),
-           "sample": f"{nb} batches x {q_np.shape[0]} queries x {x_np.shape[0]} x {x_np.shape[1]} fp32 "
-                     f"(numpy/BLAS restatement, oracle/restatement.py batched_cosine_topk)"}
-    # the reference deployment's setting: one BLAS thread (OMP_NUM_THREADS=1,
-    # docker-compose.yml:52-59), a bounded ~5 s sample
+    return len(lat), time.perf_counter() - t0, lat
+
+
+def cpu_baseline(x_np, q_np, k, budget_s=8.0, sweep_s=2.0):
+    """The oracle's batched exact cosine top-k (numpy/BLAS: the sequential-scan semantics of
+    pgvector / FAISS IndexFlat) on the host cores, timed — never extrapolated.  `value` is the
+    workload's own batch on all BLAS threads; `sweep` times B ∈ {1 (top-10, configs[0]), 256,
+    1024, 4096} on all threads and on one thread (the reference deployment's
+    OMP_NUM_THREADS=1, docker-compose.yml:52-59)."""
+    from oracle.restatement import batched_cosine_topk
+    cores = _blas_threads()
+    B = q_np.shape[0]
+    ids0 = batched_cosine_topk(x_np, q_np, k)[0]
+    nb, el, lat = _time_cpu(lambda: batched_cosine_topk(x_np, q_np, k), budget_s, 400)
+    out = {"value": round(nb * B / el, 1), "unit": "queries/s", "cores": int(cores), "kind": "port",
+           "p50_ms": round(1e3 * float(np.median(lat)), 3),
+           "sample": f"{nb} batches x {B} queries x {x_np.shape[0]} x {x_np.shape[1]} fp32 (numpy/BLAS restatement, "
+                     f"oracle/restatement.py batched_cosine_topk), timed"}
+    rng = np.random.default_rng(99)
+    qs = rng.standard_normal((4096, x_np.shape[1])).astype(np.float32)
+    sweep = []
     try:
         from threadpoolctl import threadpool_limits
-        with threadpool_limits(limits=1, user_api="blas"):
-            t0, nb1, lat1 = time.perf_counter(), 0, []
-            while nb1 < max_batches and time.perf_counter() - t0 < budget_s / 2:
-                t1 = time.perf_counter()
-                batched_cosine_topk(x_np, q_np, k)
-                lat1.append(time.perf_counter() - t1)
-                nb1 += 1
-            el1 = time.perf_counter() - t0
-        out["value_1_thread"] = round(nb1 * q_np.shape[0] / el1, 1)
-        out["p50_ms_1_thread"] = round(1e3 * float(np.median(lat1)), 3)
     except Exception:
-        pass
+        threadpool_limits = None
+    for threads in (cores, 1):
+        for b, kk in ((1, 10), (256, 50), (1024, 50), (4096, 50)):
+            qb = qs[:b]
+
+            def call():
+                batched_cosine_topk(x_np, qb, kk)
+            if threads == 1 and threadpool_limits is not None:
+                with threadpool_limits(limits=1, user_api="blas"):
+                    n_, el_, lat_ = _time_cpu(call, sweep_s, 2000)
+            elif threads == 1:
+                continue
+            else:
+                n_, el_, lat_ = _time_cpu(call, sweep_s, 2000)
+            sweep.append({"B": b, "k": kk, "threads": int(threads), "queries_per_s": round(n_ * b / el_, 1),
+                          "p50_ms": round(1e3 * float(np.median(lat_)), 3), "calls": n_})
+    out["sweep"] = sweep
+    one = [s for s in sweep if s["threads"] == 1 and s["B"] == B]
+    if one:
+        out["value_1_thread"] = one[0]["queries_per_s"]
+        out["p50_ms_1_thread"] = one[0]["p50_ms"]
     return out, ids0
 
 
@@ -129,15 +178,39 @@ SHARDED = {  # BASELINE.json configs[3] / configs[4]
 }
 
 
-def unit_rows_chunked(n, d, seed, dev, chunk=1 << 20):
-    import torch
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    out = torch.empty((n, d), dtype=torch.float32, device=dev)
-    for i in range(0, n, chunk):
-        x = torch.randn((min(chunk, n - i), d), generator=g, device=dev)
-        out[i:i + x.shape[0]] = x / x.norm(dim=1, keepdim=True)
-    return out
+def cpu_full_scan(get_chunk, n, q_np, k, budget_s=12.0, chunk=1 << 19):
+    """Timed CPU baseline over the WHOLE index (no extrapolation): the numpy/BLAS restatement
+    scanning the rows in chunks (a sequential scan, as pgvector / FAISS IndexFlat do) for a
+    bounded query sample, keeping the running exact top-k."""
+    from oracle.restatement import normalize_rows
+    qn = normalize_rows(q_np)
+    rows = [get_chunk(c0, min(n, c0 + chunk)) for c0 in range(0, n, chunk)]   # host copy, untimed
+
+    def scan(nq):
+        best_s = np.full((nq, k), -np.inf, np.float32)
+        best_i = np.zeros((nq, k), np.int64)
+        for ci, xr in enumerate(rows):
+            s = qn[:nq] @ xr.T
+            part = np.argpartition(-s, k - 1, axis=1)[:, :k]
+            cs = np.concatenate([best_s, np.take_along_axis(s, part, 1)], 1)
+            cid = np.concatenate([best_i, part + ci * chunk], 1)
+            o = np.argpartition(-cs, k - 1, axis=1)[:, :k]
+            best_s, best_i = np.take_along_axis(cs, o, 1), np.take_along_axis(cid, o, 1)
+        return best_i
+    t0 = time.perf_counter()
+    scan(1)
+    t_one = time.perf_counter() - t0
+    nq = int(max(1, min(q_np.shape[0], 64)))
+    t0 = time.perf_counter()
+    calls = 0
+    while calls < 3 and time.perf_counter() - t0 < budget_s:
+        scan(nq)
+        calls += 1
+    el = time.perf_counter() - t0
+    return {"value": round(calls * nq / el, 2), "unit": "queries/s", "cores": int(_blas_threads()), "kind": "port",
+            "p50_ms_B1": round(1e3 * t_one, 2),
+            "sample": f"{calls} batches x {nq} queries over all {n} rows x {q_np.shape[1]} (bf16 rows widened to "
+                      f"f32; numpy/BLAS chunked sequential scan), timed over the full index"}
 
 
 def run_sharded(args, rank, world, local, dev):
@@ -152,11 +225,11 @@ def run_sharded(args, rank, world, local, dev):
         os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     sh = ShardedIndex(n, dtype="bf16")
-    x = unit_rows_chunked(sh.hi - sh.lo, d, 1234 + rank, dev)   # this rank's rows only
-    sh.local.upload_items(x, prenormalized=True)
+    x = unit_rows_torch(sh.hi - sh.lo, d, 1234 + rank, dev)   # this rank's rows only
+    sh.upload_items(x, prenormalized=True)
     del x
     torch.cuda.empty_cache()
-    q = unit_rows_chunked(B, d, 4321, dev)                      # replicated batch
+    q = unit_rows_torch(B, d, 4321, dev)                      # replicated batch
 
     def step():
         return sh.search("semantic", k, q_rows=q)
@@ -170,7 +243,7 @@ def run_sharded(args, rank, world, local, dev):
     lat = []
     for _ in range(args.steps):
         t1 = time.perf_counter()
-        res = step()
+        step()
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t1)
     torch.cuda.synchronize()
@@ -179,7 +252,7 @@ def run_sharded(args, rank, world, local, dev):
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
-    # dominant kernel (the streaming scan: pilot + stream pass per step), on its own stream
+    # dominant kernel (the streaming scan: pilot + stream passes per step), on its own stream
     sh.local.set_profiling(True)
     ps = max(1, min(args.steps, 5))
     for _ in range(ps):
@@ -190,7 +263,6 @@ def run_sharded(args, rank, world, local, dev):
     n_loc = sh.hi - sh.lo
     gemm_us = 1e3 * prof["gemm"]["ms"] / ps                     # per step (all scan launches)
     flops_loc = 2.0 * B * n_loc * d
-    achieved = flops_loc / (gemm_us * 1e-6) / 1e12
     alg_bytes = n_loc * d * 2 + B * d * 4 + B * k * 8
     out = {
         "metric": f"similarity queries/sec + p50 latency, {d}-d x {n:,} items ({c['cfg'].split(':')[0]})",
@@ -200,39 +272,87 @@ def run_sharded(args, rank, world, local, dev):
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic (unit-norm N(0,1) rows, seeds 1234+rank / 4321)",
         "config": {"workload": c["cfg"], "items": n, "items_per_rank": n_loc, "dim": d, "batch": B, "top_k": k,
                    "parallelism": f"rows sharded x{world}" if world > 1 else "single"},
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_DENSE_TF, "unit": "TFLOP/s",
-                     "frac": round(achieved / BF16_DENSE_TF, 4), "traffic": None,
-                     "kernel": "scan4_kernel (pilot slab + streaming pass), per rank",
-                     "kernel_us_per_step": round(gemm_us, 1), "algorithmic_flops_per_step": flops_loc,
-                     "algorithmic_bytes_per_step": alg_bytes},
+        "roofline": roofline(flops_loc, alg_bytes, gemm_us, "bf16",
+                             "scan4_kernel (pilot slab + streaming passes), per rank, per step", 1.0,
+                             load_pmc(args.workload)),
         "kernels_us_per_step": {kk: round(1e3 * v["ms"] / ps, 2) for kk, v in prof.items() if v["launches"]},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        # bounded sample: 64 queries against the first 200K rows, scaled to the full index
-        from oracle.restatement import batched_cosine_topk
-        ns = 200_000
-        xs = sh.local.get_rows(torch.arange(ns, device=dev)).float().cpu().numpy()
-        qs = q[:64].cpu().numpy()
-        batched_cosine_topk(xs, qs[:4], k)
-        t1 = time.perf_counter()
-        nb = 0
-        while nb < 20 and time.perf_counter() - t1 < 10.0:
-            batched_cosine_topk(xs, qs, k)
-            nb += 1
-        rate = nb * 64 / (time.perf_counter() - t1) * ns / n
-        try:
-            from threadpoolctl import threadpool_info
-            cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-        except Exception:
-            cores = os.cpu_count() or 1
-        out["cpu_baseline"] = {"value": round(rate, 2), "unit": "queries/s", "cores": int(cores),
-                               "kind": "port",
-                               "sample": f"{nb} batches x 64 queries x {ns} x {d} (numpy/BLAS restatement), "
-                                         f"rate scaled by {ns}/{n} items"}
+        def get_chunk(a, b):
+            return sh.local.get_rows(torch.arange(a, b, device=dev)).float().cpu().numpy()
+        out["cpu_baseline"] = cpu_full_scan(get_chunk, n_loc, q[:64].cpu().numpy(), k)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
+
+
+def make_lane(brickrec, workload, x, B, local, dev, rank, j, dtype, inflight, extra):
+    """One in-flight lane: its own index handle (own HIP stream + workspace) and batch."""
+    import torch
+    idx = brickrec.ItemIndex(device=local, dtype=dtype)
+    idx.upload_items(x)
+    s = torch.cuda.current_stream(dev) if inflight == 1 else torch.cuda.Stream(dev)
+    if workload == "c3":
+        f, parts, year, theme = extra["f"], extra["parts"], extra["year"], extra["theme"]
+        idx.upload_cf(f)
+        idx.upload_attrs(parts, year, theme)
+        mask = idx.eval_mask(brickrec.Predicate(parts_max=800, year_min=2015))
+        rng = np.random.default_rng(7000 + rank + 10 * j)
+        liked = rng.choice(N_ITEMS, B, replace=False)
+        rated = np.zeros((B, N_ITEMS), bool)
+        for b in range(B):
+            rated[b, rng.choice(N_ITEMS, int(rng.integers(10, 31)), replace=False)] = True
+        u = rng.normal(0.0, 0.1, (B, f.shape[1])).astype(np.float32)
+        mw = torch.from_numpy(brickrec.bits_from_bool(mask).view(np.int32)).to(dev)
+        ew = torch.from_numpy(brickrec.bits_from_bool(rated).view(np.int32)).to(dev)
+        run, outs = idx.prepared_search("hybrid", TOPK, q_items=torch.from_numpy(liked).to(dev),
+                                        q_cf=torch.from_numpy(u).to(dev), mask=mw, excl=ew, stream=s)
+        return idx, s, run, outs, None
+    q = unit_rows_torch(B, DIM, 4321 + rank + 1000 * j, dev)
+    run, outs = idx.prepared_search("semantic", TOPK, q_rows=q, stream=s)
+    return idx, s, run, outs, q
+
+
+def gpu_batch_sweep(brickrec, x, local, dev, dtype, seconds=0.5):
+    """GPU q/s (3 in flight) and serial p50 at B ∈ {1 (top-10), 256, 1024, 4096}: the
+    north_star's batch axis at 25K items."""
+    import torch
+    res = []
+    for b, kk in ((1, 10), (256, 50), (1024, 50), (4096, 50)):
+        lanes = []
+        for j in range(3):
+            idx = brickrec.ItemIndex(device=local, dtype=dtype)
+            idx.upload_items(x)
+            q = unit_rows_torch(b, DIM, 555 + j, dev)
+            s = torch.cuda.Stream(dev)
+            run, _ = idx.prepared_search("semantic", kk, q_rows=q, stream=s)
+            lanes.append((idx, s, run, q))
+        for i in range(30):
+            lanes[i % 3][2]()
+        torch.cuda.synchronize()
+        steps = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            for _ in range(30):
+                lanes[steps % 3][2]()
+                steps += 1
+            torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        ser = []
+        idx0, s0, run0, _ = lanes[0]
+        for _ in range(100):
+            a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s0)
+            run0()
+            e.record(s0)
+            ser.append((a, e))
+        torch.cuda.synchronize()
+        res.append({"B": b, "k": kk, "queries_per_s_inflight3": round(steps * b / el, 1),
+                    "p50_ms_serial": round(float(np.median([a.elapsed_time(e) for a, e in ser])), 4)})
+        for ln in lanes:
+            ln[0].close()
+    return res
 
 
 def main():
@@ -241,11 +361,12 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
-    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the GPU batch sweep")
     ap.add_argument("--inflight", type=int, default=3, help="batches in flight per GPU (1 = strictly serial)")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
-                    help="c2 = configs[1] (default line); c4 / c5 = the sharded configs[3] / [4]")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
+                    help="c2 = configs[1] (default line); c3 = configs[2] hybrid; c4 / c5 = the sharded configs[3] / [4]")
     args = ap.parse_args()
 
     import torch
@@ -257,23 +378,25 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    if args.workload != "c2":
+    if args.workload in SHARDED:
         return run_sharded(args, rank, world, local, dev)
 
     import brickrec
-    B = args.batch
+    hybrid = args.workload == "c3"
+    B = args.batch or (1024 if hybrid else BATCH)
     x = unit_rows_torch(N_ITEMS, DIM, 1234, dev)              # replica of the item matrix
+    extra = {}
+    if hybrid:
+        rng = np.random.default_rng(2024)
+        extra = {"f": rng.normal(0.0, 0.1, (N_ITEMS, 50)).astype(np.float32),
+                 "parts": rng.integers(1, 6000, N_ITEMS).astype(np.int32),
+                 "year": rng.integers(1949, 2025, N_ITEMS).astype(np.int16),
+                 "theme": rng.integers(0, 400, N_ITEMS).astype(np.int32)}
     # `inflight` batches in flight: each lane is its own index handle (own HIP stream,
     # workspace and 39 MB item copy) serving its own batch; consecutive steps alternate
     # lanes, so one batch's latency-bound select overlaps the next batch's MFMA scan.
-    lanes = []
-    for j in range(args.inflight):
-        q_j = unit_rows_torch(B, DIM, 4321 + rank + 1000 * j, dev)
-        idx_j = brickrec.ItemIndex(device=local, dtype=args.dtype)
-        idx_j.upload_items(x)
-        s_j = torch.cuda.current_stream(dev) if args.inflight == 1 else torch.cuda.Stream(dev)
-        run_j, outs_j = idx_j.prepared_search("semantic", TOPK, q_rows=q_j, stream=s_j)
-        lanes.append((idx_j, s_j, run_j, outs_j, q_j))
+    lanes = [make_lane(brickrec, args.workload, x, B, local, dev, rank, j, args.dtype, args.inflight, extra)
+             for j in range(args.inflight)]
     idx, stream, run, (o_sc, o_ids, o_cnt), q = lanes[0]
 
     for i in range(args.warmup):
@@ -319,16 +442,21 @@ def main():
     prof = idx.profile()
     idx.set_profiling(False)
     g = prof["gemm"]
-    gemm_us = 1e3 * g["ms"] / max(g["launches"], 1)
-    flops = 2.0 * B * N_ITEMS * DIM
+    # all scan launches of one step (hybrid: the content and CF sides), per step
+    gemm_us = 1e3 * g["ms"] / max(args.steps, 1)
     es = 4 if args.dtype == "f32" else 2
-    alg_bytes = N_ITEMS * DIM * es + B * DIM * 4 + B * TOPK * 8    # items + queries + top-K out
-    kname, mfma_per_flop = scan_kernel_info(args.dtype)
-    bound, unit = "mfma", "TFLOP/s"
-    peak = F32_DENSE_TF if args.dtype == "f32" else BF16_DENSE_TF
-    achieved = flops / (gemm_us * 1e-6) / 1e12  # algorithmic flops per launch / launch time
-    mfma_issue_tflops = achieved * mfma_per_flop  # bf16 MFMA flops the kernel actually issues
-    hbm = load_pmc(args.dtype)
+    if hybrid:
+        r = 50
+        flops = 2.0 * B * N_ITEMS * (DIM + r)
+        alg_bytes = N_ITEMS * (DIM + r) * es + B * (r * 4 + 8) + B * TOPK * 12 + N_ITEMS // 8
+        kname, mpf = scan_kernel_info(args.dtype, DIM)
+        kname = "scan launches of one hybrid step (content d=384 + CF r=50): " + kname
+    else:
+        flops = 2.0 * B * N_ITEMS * DIM
+        alg_bytes = N_ITEMS * DIM * es + B * DIM * 4 + B * TOPK * 8    # items + queries + top-K out
+        kname, mpf = scan_kernel_info(args.dtype, DIM)
+    pmc_key = "c3" if hybrid else args.dtype
+    roof = roofline(flops, alg_bytes, gemm_us, args.dtype, kname, mpf, load_pmc(pmc_key))
 
     # ---- MALL-cold latency (256 MiB Infinity Cache flushed before each step) ----
     flush = torch.empty(640 << 20, dtype=torch.uint8, device=dev)
@@ -344,8 +472,15 @@ def main():
         cold.append(a.elapsed_time(b))
     del flush
 
+    if hybrid:
+        metric = "similarity queries/sec + p50 latency, hybrid content+CF + mask, 384-d x 25,216 items (configs[2])"
+        workload = ("configs[2]: batch=1024 hybrid (liked-set cosine top-100 + CF r=50 top-100, union blend "
+                    "0.4/0.6) + constraint mask (num_parts<=800 AND year>=2015) + rated exclusions, top-50")
+    else:
+        metric = "similarity queries/sec + p50 latency, 384-d x 25,216 items (configs[1])"
+        workload = f"configs[1]: batch={B} queries x 25,216 x 384-d items, cosine top-50"
     out = {
-        "metric": "similarity queries/sec + p50 latency, 384-d x 25,216 items (configs[1])",
+        "metric": metric,
         "value": round(world * B * args.steps / el, 1),
         "unit": "queries/s",
         "n_gpus": world,
@@ -360,23 +495,17 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (unit-norm N(0,1) rows, seeds 1234 / 4321+rank)",
-        "config": {"workload": "configs[1]: batch=256 queries x 25,216 x 384-d items, cosine top-50",
-                   "items": N_ITEMS, "dim": DIM, "batch": B, "top_k": TOPK,
+        "config": {"workload": workload, "items": N_ITEMS, "dim": DIM, "batch": B, "top_k": TOPK,
                    "parallelism": f"replicas x{world}" if world > 1 else "single",
                    "inflight_batches": args.inflight},
-        "roofline": {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-                     "frac": round(achieved / peak, 4), "traffic": hbm,
-                     "kernel": kname, "kernel_us": round(gemm_us, 3),
-                     "mfma_flops_per_algorithmic_flop": mfma_per_flop,
-                     "bf16_mfma_issue_tflops": round(mfma_issue_tflops, 2),
-                     "bf16_mfma_issue_frac": round(mfma_issue_tflops / BF16_DENSE_TF, 4),
-                     "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": alg_bytes,
-                     "hbm_frac_at_alg_bytes": round(alg_bytes / (gemm_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
+        "roofline": roof,
         "kernels_us_per_step": {k: round(1e3 * v["ms"] / max(args.steps, 1), 3) for k, v in prof.items()
                                 if v["launches"]},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_sweep and not hybrid:
+        out["gpu_batch_sweep"] = gpu_batch_sweep(brickrec, x, local, dev, args.dtype)
+    if rank == 0 and world == 1 and not args.no_cpu and not hybrid:
         x_np = x.cpu().numpy()
         q_np = q.cpu().numpy()
         cb, ids0 = cpu_baseline(x_np, q_np, TOPK)

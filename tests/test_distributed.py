@@ -58,19 +58,10 @@ def _worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_sharded_matches_unsharded(world):
+def _reference():
+    """Unsharded oracle lists per mode for _data(): semantic, similar (rank 0 dropped, mask),
+    CF (rated skipped, mask) and the hybrid union blend of their top-2k lists."""
     from oracle import restatement as R
-    ctx = mp.get_context("spawn")
-    q_ = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q_)) for r in range(world)]
-    for p in procs:
-        p.start()
-    outs = dict(q_.get(timeout=240) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
     x, f, q, u, mask, excl, items = _data()
     xn = R.normalize_rows(x.astype(np.float64)).astype(np.float32)
     ref = {}
@@ -87,6 +78,23 @@ def test_sharded_matches_unsharded(world):
         fi, fsc = R.topk_indices(fs, 2 * K, mask & ~excl[b])
         ref.setdefault("cf", []).append((fi[:K], fsc[:K]))
         ref.setdefault("hybrid", []).append(R.union_blend(ci, cs, fi, fsc, 0.4, 0.6, K))
+    return ref
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_matches_unsharded(world):
+    from oracle import restatement as R
+    ctx = mp.get_context("spawn")
+    q_ = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q_)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q_.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _reference()
     for rank in range(world):
         for mode, (sc, ids, cnt) in outs[rank].items():
             for b in range(B):

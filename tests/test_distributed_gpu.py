@@ -68,6 +68,16 @@ def test_sharded_on_device():
     for mode in outs[0]:
         for a, b_ in zip(outs[0][mode], outs[1][mode]):
             np.testing.assert_array_equal(a, b_)
+    # similar / CF / hybrid against the unsharded oracle (the device's f64-normalised rows and
+    # split-precision scores agree with the f32 oracle to ~1e-7; _data() has gaps >> that
+    # except for the duplicated rows, whose ties both sides break by id)
+    ref = T._reference()
+    for mode in ("similar", "cf", "hybrid"):
+        sc, ids, cnt = outs[0][mode]
+        for b in range(T.B):
+            ri, rs = ref[mode][b]
+            assert list(ids[b][: cnt[b]]) == list(ri), (mode, b, ids[b], ri)
+            np.testing.assert_allclose(sc[b][: cnt[b]], rs, atol=1e-5)
     # similar: the rank-0 drop crossed shards (row 0 duplicates row 3, ids tie by value)
     sc, ids, cnt = outs[0]["similar"]
     assert 0 not in ids[0][: cnt[0]]

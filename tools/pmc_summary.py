@@ -1,4 +1,6 @@
-"""Aggregate rocprofv3 counter_collection CSVs per kernel (mean per dispatch)."""
+"""Aggregate rocprofv3 counter_collection CSVs per kernel: mean per dispatch of every counter,
+plus `_dispatches` (how many dispatches of that kernel the run made, from the first counter
+seen)."""
 import csv
 import glob
 import json
@@ -13,5 +15,8 @@ for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
             name = row.get("Kernel_Name", "")
             short = name.split("(")[0].replace("void ", "")[:60]
             out[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
-res = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in out.items()}
+res = {}
+for k, d in out.items():
+    res[k] = {c: sum(v) / len(v) for c, v in d.items()}
+    res[k]["_dispatches"] = max(len(v) for v in d.values())
 print(json.dumps(res, indent=1))
