@@ -20,12 +20,13 @@ The sharded workloads (ShardedIndex: local streaming top-K, one RCCL all-gather 
 candidate keys, bb_finalize merge) fix the total items, so more GPUs means smaller shards
 ("scaling": "strong").
 
-Roofline (dominant kernel, HIP events on the library's launch stream): `achieved` is the
-MFMA work the scan kernel actually issues per second — algorithmic flops (2·B·N·d, SURVEY.md
-§8d) × the MFMA flops it executes per algorithmic flop (six bf16 products per fp32 product
-in the split-precision scan3, one for a bf16 index) — against the dense peak of that
-instruction (bf16 2.5 PF).  `f32_equivalent` prices the algorithmic flops against the f32
-MFMA peak (157.3 TF), which the split scan can exceed because it does not run on it.
+Roofline (dominant kernel = the scan launches of a step, HIP events on the library's launch
+stream; see roofline()): the binding side follows SURVEY.md §8(d), max(issued MFMA flops /
+MFMA peak, algorithmic bytes / HBM peak).  The f32 index runs the exact re-rank path (a
+one-product bf16 MFMA scan, then rerank_kernel rescores the candidates within its proven
+error bound from the f32 rows), so at configs[1] the algorithmic model binds on HBM (39.2 MB
+of f32 rows vs 4.96 GFLOP).  `f32_equivalent` prices the algorithmic flops against the f32
+MFMA peak (157.3 TF).
 
 Launch: python bench.py [--gpus 1 --steps 500 --warmup 50]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -49,34 +50,52 @@ BF16_DENSE_TF = 2500.0   # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md), no
 F32_DENSE_TF = 157.3
 
 
-def scan_kernel_info(dtype, width):
+def scan_kernel_info(dtype, width, batch):
     """(kernel, MFMA flops executed per algorithmic flop) of the scan that runs for an index
-    of this dtype and padded width.  An f32 index runs the split-precision scan3 (six bf16
-    MFMA products per fp32 product, fp32-class accuracy) unless BB_NO_SPLIT forces the fp32
-    MFMA; a bf16 index runs scan2 / scan4 on the bf16 MFMA."""
+    of this dtype and padded width on a one-slab search.  An f32 index runs the exact
+    re-rank path: a one-product bf16 MFMA scan (scan2 for up to 256 queries, scan4 above)
+    gives approximate scores within a proven bound, and rerank_kernel rescores the
+    candidates within it from the f32 rows (BB_NO_RR forces the older split-precision scan3,
+    six bf16 products per fp32 product).  A bf16 index runs scan2 / scan4 directly."""
     if os.environ.get("BB_FORCE_TILED_GEMM"):
         return "gemm_nt_kernel", 1.0
-    if dtype == "f32" and not os.environ.get("BB_NO_SPLIT"):
+    kern = "scan4_kernel" if batch > 256 else "scan2_kernel"
+    if dtype == "f32" and os.environ.get("BB_NO_RR") and not os.environ.get("BB_NO_SPLIT"):
         return f"scan3_kernel<{width * 2 // 16}> (bf16x6 split, f32 accumulate)", 6.0
-    if dtype == "f32":
+    if dtype == "f32" and os.environ.get("BB_NO_RR"):
         return "scan2_kernel<float> (fp32 MFMA)", 1.0
-    return "scan2/scan4_kernel<uint16_t> (bf16 MFMA)", 1.0
+    if dtype == "f32":
+        return (f"{kern}<uint16_t,{width * 2 // 16}> (one-product bf16 approximate scan; "
+                f"exact f32 re-rank of the candidates in rerank_kernel)"), 1.0
+    return f"{kern}<uint16_t,{width * 2 // 16}> (bf16 MFMA)", 1.0
 
 
 def roofline(flops_alg, bytes_alg, kernel_us, dtype, kname, mfma_per_flop, traffic):
-    """Roofline object of the dominant kernel: issued MFMA rate vs the issued instruction's
-    dense peak, plus the f32-equivalent pricing of the algorithmic flops."""
-    alg_tf = flops_alg / (kernel_us * 1e-6) / 1e12
+    """Roofline object of the dominant kernel.  The binding ceiling follows SURVEY.md §8(d):
+    max(issued MFMA flops / MFMA peak, algorithmic bytes / HBM peak).  `achieved` is the
+    binding side's rate: issued MFMA TFLOP/s (algorithmic flops × MFMA flops per algorithmic
+    flop) against the dense peak of the issued instruction, or algorithmic GB/s against HBM;
+    the other side is reported beside it."""
+    t = kernel_us * 1e-6
+    alg_tf = flops_alg / t / 1e12
     issued = alg_tf * mfma_per_flop
-    peak = BF16_DENSE_TF if (dtype == "bf16" or mfma_per_flop > 1) else F32_DENSE_TF
-    out = {"bound": "mfma", "achieved": round(issued, 2), "peak": peak, "unit": "TFLOP/s",
-           "frac": round(issued / peak, 4), "traffic": traffic, "kernel": kname,
-           "kernel_us": round(kernel_us, 3),
-           "achieved_is": "issued MFMA TFLOP/s = algorithmic flops x mfma_flops_per_algorithmic_flop / kernel time",
-           "mfma_flops_per_algorithmic_flop": mfma_per_flop,
-           "algorithmic_tflops": round(alg_tf, 2),
-           "algorithmic_flops_per_launch": flops_alg, "algorithmic_bytes_per_launch": bytes_alg,
-           "hbm_frac_at_alg_bytes": round(bytes_alg / (kernel_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+    peak_tf = BF16_DENSE_TF if (dtype == "bf16" or mfma_per_flop > 1 or "bf16" in kname) else F32_DENSE_TF
+    gbs = bytes_alg / t / 1e9
+    t_mfma = flops_alg * mfma_per_flop / (peak_tf * 1e12)
+    t_hbm = bytes_alg / (HBM_PEAK_GBS * 1e9)
+    if t_hbm > t_mfma:
+        out = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic}
+    else:
+        out = {"bound": "mfma", "achieved": round(issued, 2), "peak": peak_tf, "unit": "TFLOP/s",
+               "frac": round(issued / peak_tf, 4), "traffic": traffic}
+    out.update({"kernel": kname, "kernel_us": round(kernel_us, 3),
+                "ideal_us": {"mfma": round(1e6 * t_mfma, 3), "hbm": round(1e6 * t_hbm, 3)},
+                "mfma_issued_tflops": round(issued, 2), "mfma_frac": round(issued / peak_tf, 4),
+                "mfma_peak": peak_tf, "mfma_flops_per_algorithmic_flop": mfma_per_flop,
+                "algorithmic_tflops": round(alg_tf, 2), "hbm_gbs_at_alg_bytes": round(gbs, 1),
+                "hbm_frac_at_alg_bytes": round(gbs / HBM_PEAK_GBS, 4),
+                "algorithmic_flops_per_launch": flops_alg, "algorithmic_bytes_per_launch": bytes_alg})
     if dtype == "f32":
         out["f32_equivalent"] = {"achieved": round(alg_tf, 2), "peak": F32_DENSE_TF,
                                  "frac": round(alg_tf / F32_DENSE_TF, 4)}
@@ -273,7 +292,7 @@ def run_sharded(args, rank, world, local, dev):
         "config": {"workload": c["cfg"], "items": n, "items_per_rank": n_loc, "dim": d, "batch": B, "top_k": k,
                    "parallelism": f"rows sharded x{world}" if world > 1 else "single"},
         "roofline": roofline(flops_loc, alg_bytes, gemm_us, "bf16",
-                             "scan4_kernel (pilot slab + streaming passes), per rank, per step", 1.0,
+                             "scan4_kernel<uint16_t> bf16 (pilot slab + streaming passes), per rank, per step", 1.0,
                              load_pmc(args.workload)),
         "kernels_us_per_step": {kk: round(1e3 * v["ms"] / ps, 2) for kk, v in prof.items() if v["launches"]},
         "cpu_baseline": None,
@@ -449,12 +468,12 @@ def main():
         r = 50
         flops = 2.0 * B * N_ITEMS * (DIM + r)
         alg_bytes = N_ITEMS * (DIM + r) * es + B * (r * 4 + 8) + B * TOPK * 12 + N_ITEMS // 8
-        kname, mpf = scan_kernel_info(args.dtype, DIM)
+        kname, mpf = scan_kernel_info(args.dtype, DIM, B)
         kname = "scan launches of one hybrid step (content d=384 + CF r=50): " + kname
     else:
         flops = 2.0 * B * N_ITEMS * DIM
         alg_bytes = N_ITEMS * DIM * es + B * DIM * 4 + B * TOPK * 8    # items + queries + top-K out
-        kname, mpf = scan_kernel_info(args.dtype, DIM)
+        kname, mpf = scan_kernel_info(args.dtype, DIM, B)
     pmc_key = "c3" if hybrid else args.dtype
     roof = roofline(flops, alg_bytes, gemm_us, args.dtype, kname, mpf, load_pmc(pmc_key))
 

@@ -41,8 +41,8 @@ int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 size_t elem_size(int dtype) { return dtype == F64 ? 8 : dtype == BF16 ? 2 : 4; }
 
 // K_RERUN counts searches the streaming path handed back to the slab path (no kernel time)
-enum Kfam { K_PREP = 0, K_GEMM = 1, K_SELECT = 2, K_FIN = 3, K_MASK = 4, K_RERUN = 5, K_NFAM = 6 };
-const char* kFamNames[K_NFAM] = {"prep", "gemm", "select", "finalize", "mask", "rerun"};
+enum Kfam { K_PREP = 0, K_GEMM = 1, K_SELECT = 2, K_FIN = 3, K_MASK = 4, K_RERUN = 5, K_RERANK = 6, K_NFAM = 7 };
+const char* kFamNames[K_NFAM] = {"prep", "gemm", "select", "finalize", "mask", "rerun", "rerank"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -97,10 +97,16 @@ struct bb_index {
   int r = 0, Rpad = 0;
   DevBuf cf, cf_present;
   DevBuf items3, cf3;  // f32 index: the same rows as three bf16 planes (split scan, scan3)
+  // f32 index: one-product bf16 copies for the approximate scan of the exact re-rank path
+  // ([Npad][Dpad_b] / [Npad][Rpad_b]) and their error statistics (rr_prepare_kernel)
+  DevBuf items_bf, cf_bf, rr_stats;
+  int Dpad_b = 0, Rpad_b = 0;
   DevBuf parts, year, theme;
 
   // workspace
   DevBuf qn, qcf, S, tmax, keys, maxk, stage_in, out_sc, out_id, out_cnt, tmp;
+  DevBuf qf32, qeps, qcf32, qcfeps;  // re-rank: f32 query rows and per-query bounds
+  DevBuf rr_out, rr_cnt, rr_thr, rr_r0, rr_r0n;  // re-rank: select -> rerank hand-off
   // streaming top-K (large indexes): pilot lists, candidate regions, overflow flag
   DevBuf pilot, cand, cand_cnt, cand_pmax, ovf;
   DevBuf list1, max1;  // two-level streaming: exact top-K_int (+ rank-0 key) of items [0, n1)
@@ -261,7 +267,9 @@ int bb_destroy(bb_index* x) {
     }
     for (DevBuf* b : {&x->items, &x->items_present, &x->ones, &x->zeros, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S, &x->tmax,
                       &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
-                      &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3})
+                      &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
+                      &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->rr_out, &x->rr_cnt,
+                      &x->rr_thr, &x->rr_r0, &x->rr_r0n})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
     if (x->has_last) (void)hipEventSynchronize(x->done);
@@ -355,6 +363,26 @@ static int make_planes(bb_index* x, DevBuf& rows, DevBuf& planes, int ld) {
   return BB_OK;
 }
 
+// f32 index: the one-product bf16 copy + error statistics for the exact re-rank path (the
+// approximate bf16 MFMA scan, then the f32 rescoring of the candidates within its bound).
+// stat_off: 0 = item rows, 4 = CF factors.  Widths the bf16 scan or the re-rank cannot take
+// leave the copy unset (those searches run the split-precision scan instead).
+static int make_rr(bb_index* x, DevBuf& rows, DevBuf& bf, int ld, int& ld_b, int stat_off) {
+  ld_b = (int)round_up(ld, 64);
+  if (x->dtype != F32 || ld > kRrMaxD || !gemm_uses_scan(BF16, kTileRows, ld_b)) {
+    bf.release();
+    ld_b = 0;
+    return BB_OK;
+  }
+  int rc;
+  if ((rc = bf.ensure((size_t)x->Npad * ld_b * 2)) || (rc = x->rr_stats.ensure(64))) return rc;
+  BB_HIP(hipMemsetAsync((float*)x->rr_stats.p + stat_off, 0, 16, x->stream));
+  BB_HIP(launch_rr_prepare((const float*)rows.p, x->Npad, ld, (uint16_t*)bf.p, ld_b, (float*)x->rr_stats.p + stat_off,
+                           x->stream));
+  BB_HIP(hipStreamSynchronize(x->stream));
+  return BB_OK;
+}
+
 int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t in_dtype, int32_t prenormalized,
                     int32_t where, const uint32_t* present_bits) {
   if (!x || !rows || n <= 0 || d <= 0) return fail(BB_E_ARG, "bb_upload_items: bad arguments");
@@ -385,6 +413,7 @@ int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t
   BB_HIP(hipMemsetAsync(x->zeros.p, 0, wbytes, x->stream));
   if ((rc = upload_rows(x, rows, n, d, in_dtype, prenormalized ? 0 : 1, where, x->items.p, x->Dpad))) return rc;
   if ((rc = make_planes(x, x->items, x->items3, x->Dpad))) return rc;
+  if ((rc = make_rr(x, x->items, x->items_bf, x->Dpad, x->Dpad_b, 0))) return rc;
   return leave_stream(x, x->stream);
 }
 
@@ -411,6 +440,7 @@ int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const 
   }
   if ((rc = upload_rows(x, f, x->n, r, in_dtype, 0, BB_HOST, x->cf.p, x->Rpad))) return rc;
   if ((rc = make_planes(x, x->cf, x->cf3, x->Rpad))) return rc;
+  if ((rc = make_rr(x, x->cf, x->cf_bf, x->Rpad, x->Rpad_b, 4))) return rc;
   return leave_stream(x, x->stream);
 }
 
@@ -544,6 +574,12 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   const int64_t slab = lds;        // multiple of kTileRows
   const int64_t n_slabs = (x->n + slab - 1) / slab;
   const int64_t ldt = slab / 32;   // per-tile maxima per query row
+  // exact re-rank path (f32 index, one slab): the one-product bf16 MFMA scan writes
+  // approximate scores, the select rescores the candidates within their error bound from
+  // the f32 rows.  BB_NO_RR (A/B runs) forces the split-precision scan instead.
+  static const bool no_rr = getenv("BB_NO_RR") != nullptr;
+  const bool rr_c = !no_rr && !stream && n_slabs == 1 && need_content && x->items_bf.p;
+  const bool rr_f = !no_rr && !stream && n_slabs == 1 && need_cf && x->cf_bf.p;
 
   // stage host inputs
   const size_t es_q = elem_size(q->q_dtype), es_cf = elem_size(q->q_cf_dtype);
@@ -570,8 +606,15 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   if ((rc = x->tmax.ensure((size_t)Bc * ldt * 4 * 2))) return rc;  // tmax + pmax
   // query rows: index dtype, or three bf16 planes (6 B / element) for the split scan
   const size_t qes_c = x->items3.p ? std::max<size_t>(es, 6) : es, qes_f = x->cf3.p ? std::max<size_t>(es, 6) : es;
-  if (need_content && (rc = x->qn.ensure((size_t)Bc * x->Dpad * qes_c))) return rc;
-  if (need_cf && (rc = x->qcf.ensure((size_t)Bc * x->Rpad * qes_f))) return rc;
+  if (need_content && (rc = x->qn.ensure(std::max((size_t)Bc * x->Dpad * qes_c, (size_t)Bc * x->Dpad_b * 2)))) return rc;
+  if (need_cf && (rc = x->qcf.ensure(std::max((size_t)Bc * x->Rpad * qes_f, (size_t)Bc * x->Rpad_b * 2)))) return rc;
+  if (rr_c && ((rc = x->qf32.ensure((size_t)Bc * x->Dpad * 4)) || (rc = x->qeps.ensure((size_t)Bc * 4)))) return rc;
+  if (rr_f && ((rc = x->qcf32.ensure((size_t)Bc * x->Rpad * 4)) || (rc = x->qcfeps.ensure((size_t)Bc * 4)))) return rc;
+  if ((rr_c || rr_f) &&
+      ((rc = x->rr_out.ensure((size_t)Bc * kRrCap * 8)) || (rc = x->rr_cnt.ensure((size_t)Bc * 4)) ||
+       (rc = x->rr_thr.ensure((size_t)Bc * 8)) || (rc = x->rr_r0.ensure((size_t)Bc * kRrR0Cap * 4)) ||
+       (rc = x->rr_r0n.ensure((size_t)Bc * 4))))
+    return rc;
   const size_t side_keys = (size_t)Bc * K_int;
   if ((rc = x->keys.ensure(2 * sides * side_keys * 8))) return rc;
   if ((rc = x->maxk.ensure((size_t)Bc * 8))) return rc;
@@ -653,10 +696,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // rows; raw f32 rows with 16-B rows), otherwise a prep launch fills qn / qcf ----
     // split-precision scan (f32 index with bf16 planes): queries always come from a prep
     // launch writing the q3f plane image (coalesced query loads in the scan)
-    const bool s3_c = need_content && x->items3.p && scan3_supported(bpad, x->Dpad);
-    const bool s3_f = need_cf && x->cf3.p && scan3_supported(bpad, x->Rpad);
-    const bool scan_c = !s3_c && gemm_uses_scan(x->dtype, bpad, x->Dpad);
-    const bool scan_f = !s3_f && need_cf && gemm_uses_scan(x->dtype, bpad, x->Rpad);
+    const bool s3_c = !rr_c && need_content && x->items3.p && scan3_supported(bpad, x->Dpad);
+    const bool s3_f = !rr_f && need_cf && x->cf3.p && scan3_supported(bpad, x->Rpad);
+    const bool scan_c = !rr_c && !s3_c && gemm_uses_scan(x->dtype, bpad, x->Dpad);
+    const bool scan_f = !rr_f && !s3_f && need_cf && gemm_uses_scan(x->dtype, bpad, x->Rpad);
     const bool gather_c = q->mode != BB_MODE_SEMANTIC && d_items;
     const float* rows_c = d_rows ? (const float*)((const char*)d_rows + (size_t)b0 * x->d * es_q) : nullptr;
     const float* rows_f = d_cf ? (const float*)((const char*)d_cf + (size_t)b0 * x->r * es_cf) : nullptr;
@@ -674,6 +717,14 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       pa.Dpad = x->Dpad;
       pa.out = x->qn.p;
       pa.out_dtype = s3_c ? SPLIT3 : x->dtype;
+      if (rr_c) {  // bf16 operand + f32 row + bound
+        pa.out_dtype = BF16;
+        pa.Dpad = x->Dpad_b;
+        pa.out_f32 = (float*)x->qf32.p;
+        pa.Dpad_f = x->Dpad;
+        pa.eps_out = (float*)x->qeps.p;
+        pa.istats = (const float*)x->rr_stats.p;
+      }
       pa.items = x->items.p;
       pa.n_items = x->n;
       pa.id_offset = x->id_offset;
@@ -695,6 +746,14 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       pa.Dpad = x->Rpad;
       pa.out = x->qcf.p;
       pa.out_dtype = s3_f ? SPLIT3 : x->dtype;
+      if (rr_f) {
+        pa.out_dtype = BF16;
+        pa.Dpad = x->Rpad_b;
+        pa.out_f32 = (float*)x->qcf32.p;
+        pa.Dpad_f = x->Rpad;
+        pa.eps_out = (float*)x->qcfeps.p;
+        pa.istats = (const float*)x->rr_stats.p + 4;
+      }
       pa.src = (const char*)d_cf + (size_t)b0 * x->r * es_cf;
       pa.src_dtype = q->q_cf_dtype;
       pa.src_ld = x->r;
@@ -766,7 +825,15 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           }
         }
         DevBuf& planes = cf_side ? x->cf3 : x->items3;
-        if (cf_side ? s3_f : s3_c) {
+        const bool rr_side = cf_side ? rr_f : rr_c;
+        if (rr_side) {
+          // approximate scan: bf16 queries x the one-product bf16 item copy
+          const int64_t w = cf_side ? x->Rpad_b : x->Dpad_b;
+          ga.X = (const char*)(cf_side ? x->cf_bf.p : x->items_bf.p) + (size_t)c0 * w * 2;
+          ga.ldx = ga.ldq = w;
+          ga.Kpad = (int)w;
+          if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(BF16, ga, s); }))) return rc;
+        } else if (cf_side ? s3_f : s3_c) {
           // split-precision scan: items, gathered rows and prepped queries are bf16 planes
           const int64_t w = ga.ldq;
           ga.X = (const char*)planes.p + (size_t)c0 * 3 * w * 2;
@@ -825,7 +892,21 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         sa.K = K_int;
         // blocked score image: the split scan, and the bf16 scan with 64 queries per wave
         sa.s_blocked = ((cf_side ? s3_f : s3_c) ||
-                        ((cf_side ? scan_f : scan_c) && scan4_used(x->dtype, bpad))) ? 1 : 0;
+                        ((cf_side ? scan_f : scan_c) && scan4_used(x->dtype, bpad)) ||
+                        (rr_side && scan4_used(BF16, bpad))) ? 1 : 0;
+        if (rr_side) {
+          sa.rr_eps = (const float*)(cf_side ? x->qcfeps.p : x->qeps.p);
+          sa.rr_x = (const float*)(cf_side ? x->cf.p : x->items.p);
+          sa.rr_q = (const float*)(cf_side ? x->qcf32.p : x->qf32.p);
+          sa.rr_ld = cf_side ? x->Rpad : x->Dpad;
+          sa.rr_d = (int)sa.rr_ld;
+          sa.rr_gid_base = (uint32_t)x->id_offset;
+          sa.rr_out = (uint64_t*)x->rr_out.p;
+          sa.rr_cnt = (uint32_t*)x->rr_cnt.p;
+          sa.rr_thr = (uint32_t*)x->rr_thr.p;
+          sa.rr_r0 = (uint32_t*)x->rr_r0.p;
+          sa.rr_r0n = (uint32_t*)x->rr_r0n.p;
+        }
         sa.carry_in = sl && !stream ? keys + ((size_t)(pp ^ 1) * sides + side) * side_keys : nullptr;
         sa.keys_out = pilot ? (uint64_t*)x->pilot.p : keys + ((size_t)pp * sides + side) * side_keys;
         sa.max_inout = side_drop && !pilot ? maxk : nullptr;
@@ -838,6 +919,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           sa.k_final = q->k;
         }
         if ((rc = timed(x, K_SELECT, s, [&] { return launch_select(sa, bc, s); }))) return rc;
+        if (rr_side && (rc = timed(x, K_RERANK, s, [&] { return launch_rerank(sa, bc, s); }))) return rc;
         final_pp = pp;
       }
     }

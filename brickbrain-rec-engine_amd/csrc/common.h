@@ -133,7 +133,27 @@ struct SelectArgs {
   int32_t k_final;
   int32_t s_blocked;        // S is the scan3 blocked image (sblk_quad), else row-major [B][lds]
   uint64_t* trace;          // probe builds only: per-workgroup phase timestamps, or null
+  // exact re-rank of an approximate (one-product bf16 MFMA) score slab (rr_eps != null):
+  // every S value is within rr_eps[row] of the exact score x·q of the f32 rows, so the
+  // items whose approximate score reaches (K-th approximate) − 2ε hold the exact top-K;
+  // they are rescored from the f32 rows (f64 sum, rounded to f32) and ranked by that.
+  const float* rr_eps;      // [B] per-query bound ε, or null (S is exact)
+  const float* rr_x;        // f32 item rows [Npad][rr_ld]; local row = gid - rr_gid_base
+  const float* rr_q;        // f32 query rows [B][rr_ld]
+  int64_t rr_ld;
+  int32_t rr_d;             // elements of a row to dot (multiple of 4, <= rr_ld)
+  uint32_t rr_gid_base;     // global id of local row 0 (the index's id_offset)
+  // hand-off from select_kernel to rerank_kernel
+  uint64_t* rr_out;         // [B][kRrCap] approximate candidate keys within 2ε of the K-th
+  uint32_t* rr_cnt;         // [B] candidates, or kRrSlow (masses at the bound: exact slow path)
+  uint32_t* rr_thr;         // [B][2] order images: gather bound (slow path), rank-0 bound
+  uint32_t* rr_r0;          // [B][kRrR0Cap] rank-0 candidate global ids
+  uint32_t* rr_r0n;         // [B] their count, or kRrSlow
 };
+constexpr int kRrCap = 512;
+constexpr int kRrR0Cap = 64;
+constexpr int kRrMaxD = 512;   // widest f32 row the re-rank takes (wider: the split scan)
+constexpr uint32_t kRrSlow = 0xFFFFFFFFu;
 
 // Streaming top-K, second stage: per query, the exact top-K (full key order) of the
 // candidates the streaming scan appended to the query's regions.
@@ -182,6 +202,13 @@ struct PrepArgs {
   void* out;                // [Bpad][Dpad] index dtype
   int32_t out_dtype;
   int32_t B, Bpad;
+  // re-rank operands (out_dtype == BF16 with out_f32 set): the f32 row [Bpad][Dpad_f] beside
+  // the bf16 operand, and the per-row bound ε of |bf16 dot − f32 dot| against items whose
+  // error statistics are istats (rr_prepare_kernel): ε = E_x·|q̃| + N_x·|q̃−q| + γ·Ñ_x·|q̃|
+  float* out_f32;
+  int32_t Dpad_f;
+  float* eps_out;           // [Bpad]
+  const float* istats;      // [3]: max |x̃−x|, max |x|, max |x̃| over the item rows
 };
 
 struct MaskArgs {
@@ -205,10 +232,15 @@ int scan_chunks(int dtype, int Mpad, int tiles, bool split);
 bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s);  // scan4_used(BF16, a.Mpad) shapes
 hipError_t launch_scan3(const GemmArgs& a, hipStream_t s);  // X = item planes, Q = q3f image
 hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t* dst, hipStream_t s);
+// f32 rows [Npad][ld_f] -> bf16 copy [Npad][ld_b] (RNE, zero padded) + error statistics
+// stats[0..2] = max over rows of |x̃−x|, |x|, |x̃| (rounded up; stats must start at 0)
+hipError_t launch_rr_prepare(const float* src, int64_t npad, int64_t ld_f, uint16_t* dst, int64_t ld_b,
+                             float* stats, hipStream_t s);
 int gemm_tile_m(int dtype);
 int gemm_tile_n(int dtype);
 int gemm_tile_k(int dtype);
 hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s);
+hipError_t launch_rerank(const SelectArgs& a, int B, hipStream_t s);  // after launch_select, rr_* set
 hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s);

@@ -126,6 +126,48 @@ hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t
 }
 
 // ---------------------------------------------------------------------------------------
+// Re-rank operands of an f32 index: the one-product bf16 copy of every row (RNE) for the
+// approximate MFMA scan, and the statistics that bound its error (prep_kernel turns them
+// into the per-query ε): max over rows of ||x̃−x||, ||x||, ||x̃|| (f64 sums, rounded up to
+// f32, merged by integer atomicMax — non-negative floats order like their bit patterns).
+// One wave per row.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rr_prepare_kernel(const float* src, int64_t npad, int64_t ld_f, uint16_t* dst,
+                                                         int64_t ld_b, float* stats) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= npad) return;
+  double e2 = 0.0, n2 = 0.0, b2 = 0.0;
+  for (int64_t i = lane; i < ld_b; i += 64) {
+    const float v = i < ld_f ? src[row * ld_f + i] : 0.f;
+    const uint16_t hb = to_bf16(v);
+    const float bv = __builtin_bit_cast(float, (uint32_t)hb << 16);
+    dst[row * ld_b + i] = hb;
+    const double dv = (double)v, db = (double)bv;
+    e2 += (dv - db) * (dv - db);
+    n2 += dv * dv;
+    b2 += db * db;
+  }
+  e2 = wave_sum(e2);
+  n2 = wave_sum(n2);
+  b2 = wave_sum(b2);
+  if (lane == 0) {
+    atomicMax((unsigned int*)&stats[0], __float_as_uint(__double2float_ru(sqrt(e2))));
+    atomicMax((unsigned int*)&stats[1], __float_as_uint(__double2float_ru(sqrt(n2))));
+    atomicMax((unsigned int*)&stats[2], __float_as_uint(__double2float_ru(sqrt(b2))));
+  }
+}
+
+hipError_t launch_rr_prepare(const float* src, int64_t npad, int64_t ld_f, uint16_t* dst, int64_t ld_b, float* stats,
+                             hipStream_t s) {
+  if (npad <= 0) return hipSuccess;
+  if (ld_b < ld_f) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rr_prepare_kernel, dim3((unsigned)((npad + 3) / 4)), dim3(256), 0, s, src, npad, ld_f, dst, ld_b,
+                     stats);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // query preparation: normalise query rows (semantic), or gather the stored (already
 // normalised) item rows of the liked sets (similar-sets: the query IS feat_matrix[target],
 // recommendation_system.py:213), or copy user factor rows (CF, :435).  Rows >= B are zero.
@@ -181,6 +223,27 @@ __device__ __forceinline__ void store_q(const PrepArgs& a, int row, int i, float
   }
 }
 
+// Re-rank outputs of one query row (PrepArgs.out_f32): the f32 element beside the bf16
+// operand, and ε = E_x·|q̃| + N_x·|q̃−q| + γ·Ñ_x·|q̃| — Cauchy-Schwarz on
+// Σ(x̃−x)q̃ + Σx(q̃−q), plus γ = 2·Dpad·2^-24 for the MFMA's f32 accumulation of Σx̃q̃.
+struct RrAcc {
+  double e2 = 0.0, b2 = 0.0;
+  __device__ __forceinline__ void add(const PrepArgs& a, int row, int i, float v) {
+    if (i < a.Dpad_f) a.out_f32[(size_t)row * a.Dpad_f + i] = v;
+    const double bv = (double)__builtin_bit_cast(float, (uint32_t)to_bf16(v) << 16);
+    e2 += ((double)v - bv) * ((double)v - bv);
+    b2 += bv * bv;
+  }
+  __device__ __forceinline__ void finish(const PrepArgs& a, int row, int lane) {
+    const double e = sqrt(wave_sum(e2)), b = sqrt(wave_sum(b2));
+    if (lane == 0) {
+      const double gam = 2.0 * (double)a.Dpad * 0x1p-24;
+      const double eps = (double)a.istats[0] * b + (double)a.istats[1] * e + gam * (double)a.istats[2] * b;
+      a.eps_out[row] = __double2float_ru(eps * (1.0 + 0x1p-20));
+    }
+  }
+};
+
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -193,15 +256,20 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     const int64_t lid = a.item_ids[row] - a.id_offset;
     zero = !(lid >= 0 && lid < a.n_items);
     src = a.items;
-    sdt = a.out_dtype == SPLIT3 ? F32 : a.out_dtype;
-    d = a.Dpad;
+    sdt = a.out_dtype == SPLIT3 || a.out_f32 ? F32 : a.out_dtype;
+    d = a.out_f32 ? a.Dpad_f : a.Dpad;   // re-rank: the f32 rows (stride Dpad_f)
     norm_on = 0;
-    sb = zero ? 0 : (size_t)lid * a.Dpad;
+    sb = zero ? 0 : (size_t)lid * d;
   }
   if (zero) {
     for (int i = lane; i < a.Dpad; i += 64) store_q(a, row, i, 0.f);
+    if (a.out_f32) {
+      for (int i = lane; i < a.Dpad_f; i += 64) a.out_f32[(size_t)row * a.Dpad_f + i] = 0.f;
+      if (lane == 0) a.eps_out[row] = 0.f;
+    }
     return;
   }
+  RrAcc rr;
   if (a.Dpad <= 64 * kPrepC) {
     double x[kPrepC];
     load_chunk<kPrepC>(src, sdt, sb, 0, d, lane, x);
@@ -217,8 +285,13 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
 #pragma unroll
     for (int c = 0; c < kPrepC; ++c) {
       const int i = lane + 64 * c;
-      if (i < a.Dpad) store_q(a, row, i, (float)(x[c] / norm));
+      if (i < a.Dpad) {
+        const float v = (float)(x[c] / norm);
+        store_q(a, row, i, v);
+        if (a.out_f32) rr.add(a, row, i, v);
+      }
     }
+    if (a.out_f32) rr.finish(a, row, lane);
     return;
   }
   double norm = 1.0;
@@ -240,9 +313,14 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
 #pragma unroll
     for (int c = 0; c < kPrepC; ++c) {
       const int i = base + lane + 64 * c;
-      if (i < a.Dpad) store_q(a, row, i, (float)(x[c] / norm));
+      if (i < a.Dpad) {
+        const float v = (float)(x[c] / norm);
+        store_q(a, row, i, v);
+        if (a.out_f32) rr.add(a, row, i, v);
+      }
     }
   }
+  if (a.out_f32) rr.finish(a, row, lane);
 }
 
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s) {

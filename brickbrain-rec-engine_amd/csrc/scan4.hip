@@ -11,8 +11,14 @@ static bool scan4_env_off() {
   return off;
 }
 
-// bf16 index, query rows padded to whole 256-query groups: the 64-queries-per-wave scan
-bool scan4_used(int dtype, int Mpad) { return dtype == BF16 && Mpad % kScan4Queries == 0 && !scan4_env_off(); }
+// bf16 scan, query rows padded to whole 256-query groups and at least BB_SCAN4_MIN rows
+// (default 512): the 64-queries-per-wave scan.  A single 256-query group runs scan2
+// (measured at 25,216 x 384, B=256: 20.5 vs 23.6 us per launch, 13.3M vs 7.4M q/s with
+// three batches in flight, profiles/r02c_b2.jsonl).
+bool scan4_used(int dtype, int Mpad) {
+  static const int min_rows = getenv("BB_SCAN4_MIN") ? atoi(getenv("BB_SCAN4_MIN")) : 512;
+  return dtype == BF16 && Mpad % kScan4Queries == 0 && Mpad >= min_rows && !scan4_env_off();
+}
 
 int scan_chunks(int dtype, int Mpad, int tiles, bool split) {
   return !split && scan4_used(dtype, Mpad) ? scan4_n_chunks(Mpad, tiles) : scan_n_chunks(Mpad, tiles);

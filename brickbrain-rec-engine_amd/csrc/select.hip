@@ -32,7 +32,9 @@ constexpr int kOffTmax = kRegionA;              // u32[256] per-thread maxima
 constexpr int kTileCap = 1024;                  // qualifying-tile list capacity
 constexpr int kOffTlist = kOffTmax + kSelectThreads * 4;
 constexpr int kOffMisc = kOffTlist + kTileCap * 4;
-constexpr int kSelectLds = kOffMisc + 256;
+constexpr int kOffR0 = kOffMisc + 256;          // re-rank: rank-0 tile list
+constexpr int kR0Cap = 32;
+constexpr int kSelectLds = kOffR0 + kR0Cap * 4;
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -284,6 +286,157 @@ __device__ void wave_sort_emit(const uint64_t* cand, int cnt, const SelectArgs& 
   for (int e = 64 * E + lane; e < a.K; e += 64) out[e] = 0ull;
 }
 
+// ---- exact re-rank helpers (SelectArgs.rr_*) ----------------------------------------------
+// Margin between an approximate score and the exact one, both ways: 2ε plus slack for the
+// f32 evaluation of ε and for ties created by rounding the exact f64 sums to f32.
+__device__ __forceinline__ float rr_margin(float eps) { return eps > 0.f ? 2.f * eps * (1.f + 0x1p-10f) + 0x1p-20f : 0.f; }
+// ord image of (score(o) − m), rounded down; never below 1 (1 = "every eligible item")
+__device__ __forceinline__ uint32_t ord_sub(uint32_t o, float m) {
+  if (o <= 1u || m <= 0.f) return o;
+  const float g = __double2float_rd((double)float_of_ord(o) - (double)m);
+  const uint32_t r = ord_of(g);
+  return r > 1u ? r : 1u;
+}
+// Exact score of one item row against the query row: f32 products summed in f64 as 16
+// lane partials (partial p takes float4 chunks p, p+16, ... in order) combined by the xor
+// tree of 8, 4, 2, 1 — one fixed order, so every path (grouped or per-thread) gives the
+// same bits.  Loads are issued unconditionally (clamped index, masked contribution) so all
+// of a row's chunks are in flight together.
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4v lds_f4(const float* qs, int c) {
+  return *(const __attribute__((address_space(3))) f4v*)((const __attribute__((address_space(3))) char*)
+                                                            ((size_t)(const void*)qs) + c * 16);
+}
+__device__ __forceinline__ double fma4(const f4v& x, const f4v& q, double acc) {
+  acc = fma((double)x.x, (double)q.x, acc);
+  acc = fma((double)x.y, (double)q.y, acc);
+  acc = fma((double)x.z, (double)q.z, acc);
+  return fma((double)x.w, (double)q.w, acc);
+}
+__device__ __forceinline__ float rr_dot_thread(const float* xrow, const float* qs, int nch) {
+  const f4v* xr = (const f4v*)xrow;
+  double s[16];
+#pragma unroll
+  for (int p = 0; p < 16; ++p) s[p] = 0.0;
+  for (int base = 0; base < nch; base += 16) {
+#pragma unroll
+    for (int h = 0; h < 16; h += 8) {   // 8 chunks in flight: partials h..h+7
+      f4v xv[8];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) xv[p] = xr[min(base + h + p, nch - 1)];
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        if (base + h + p < nch) s[h + p] = fma4(xv[p], lds_f4(qs, base + h + p), s[h + p]);
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1)
+#pragma unroll
+    for (int p = 0; p < o; ++p) s[p] = s[p] + s[p + o];
+  return (float)s[0];
+}
+__device__ __forceinline__ uint64_t rr_key(float e, uint32_t gid) { return make_key(ord_of(e + 0.0f), gid); }
+
+// Rescore keys[0..m) in place (approximate -> exact keys): 16 lanes per candidate, each
+// group with U candidates' rows in flight at once; the query chunks of the lane stay in
+// registers.
+template <int CPL>
+__device__ void rr_rescore(uint64_t* keys, int m, const SelectArgs& a, const float* qs) {
+  constexpr int U = CPL <= 6 ? 4 : CPL <= 8 ? 2 : 1;  // <= 24 row chunks in flight per lane
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int p = lane & 15, g = wave * 4 + (lane >> 4);   // 16 groups per workgroup
+  const int nch = a.rr_d >> 2;
+  f4v qv[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = p + 16 * j;
+    qv[j] = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int c0 = g * U; c0 < m; c0 += 16 * U) {
+    uint32_t gid[U];
+    f4v xv[U][CPL];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      gid[u] = c0 + u < m ? gid_of(keys[c0 + u]) : a.rr_gid_base;
+      const f4v* xr = (const f4v*)(a.rr_x + (size_t)(gid[u] - a.rr_gid_base) * a.rr_ld);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) xv[u][j] = xr[min(p + 16 * j, nch - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j)
+        if (p + 16 * j < nch) acc = fma4(xv[u][j], qv[j], acc);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+      if (p == 0 && c0 + u < m) keys[c0 + u] = rr_key((float)acc, gid[u]);
+    }
+  }
+}
+__device__ __forceinline__ void rr_rescore_any(uint64_t* keys, int m, const SelectArgs& a, const float* qs) {
+  const int cpl = ((a.rr_d >> 2) + 15) >> 4;
+  if (cpl <= 2) rr_rescore<2>(keys, m, a, qs);
+  else if (cpl <= 4) rr_rescore<4>(keys, m, a, qs);
+  else if (cpl <= 6) rr_rescore<6>(keys, m, a, qs);
+  else rr_rescore<8>(keys, m, a, qs);   // rows up to kRrMaxD = 512 wide
+}
+
+// Re-rank with masses of items at the gather bound (more than kCandCap): an exact running
+// top-K over every eligible item whose approximate score reaches Tg, rescored one item per
+// thread and merged into the list 1024+ keys at a time; then the final list / key list.
+template <typename Elig, typename SAt>
+__device__ void rr_slow_path(const SelectArgs& a, int row, int n, uint32_t Tg, int K, uint64_t* cand, uint32_t* misc,
+                             const float* qs, Elig elig, SAt s_at) {
+  const int tid = threadIdx.x;
+  uint64_t* sel = cand + 2048;  // the running list: K <= kMaxKInt keys, sorted desc
+  uint64_t* buf = cand;         // fresh keys [0, nb) + the list appended for the merge
+  for (int i = tid; i < K; i += kSelectThreads) sel[i] = 0ull;
+  if (tid == 0) misc[12] = 0;
+  __syncthreads();
+  auto merge = [&]() {
+    const int nb = (int)misc[12];
+    for (int i = tid; i < K; i += kSelectThreads) buf[nb + i] = sel[i];
+    int P = 1;
+    while (P < nb + K) P <<= 1;
+    for (int i = nb + K + tid; i < P; i += kSelectThreads) buf[i] = 0ull;
+    __syncthreads();
+    bitonic_desc_u64(buf, P);
+    for (int i = tid; i < K; i += kSelectThreads) sel[i] = buf[i];
+    __syncthreads();
+    if (tid == 0) misc[12] = 0;
+    __syncthreads();
+  };
+  for (int base = 0; base < n; base += kSelectThreads) {
+    const int j = base + tid;
+    if (j < n && ((elig(j >> 5) >> (j & 31)) & 1u) && ord_of(s_at(j)) >= Tg) {
+      const uint32_t gid = a.gid0 + (uint32_t)j;
+      const uint64_t k = rr_key(rr_dot_thread(a.rr_x + (size_t)(gid - a.rr_gid_base) * a.rr_ld, qs, a.rr_d >> 2), gid);
+      buf[atomicAdd(&misc[12], 1u)] = k;
+    }
+    __syncthreads();
+    if (misc[12] > 2048u - kMaxKInt - kSelectThreads) merge();
+  }
+  if (misc[12]) merge();
+  const uint64_t gmax = *(const uint64_t*)(misc + 10);
+  int cnt = 0;
+  for (int i = 0; i < K; ++i) cnt += sel[i] != 0ull;  // uniform: every thread counts
+  if (a.out_scores) {
+    const int start = (gmax && cnt && sel[0] == gmax) ? 1 : 0;
+    const int c = min(a.k_final, cnt - start);
+    float* sc = a.out_scores + (size_t)row * a.k_final;
+    int64_t* id = a.out_ids + (size_t)row * a.k_final;
+    for (int i = tid; i < a.k_final; i += kSelectThreads) {
+      sc[i] = i < c ? float_of_ord(ordk_of(sel[start + i])) : 0.f;
+      id[i] = i < c ? (int64_t)gid_of(sel[start + i]) : (int64_t)-1;
+    }
+    if (a.out_counts && tid == 0) a.out_counts[row] = c;
+    return;
+  }
+  uint64_t* out = a.keys_out + (size_t)row * K;
+  for (int i = tid; i < K; i += kSelectThreads) out[i] = sel[i];
+}
+
 __device__ const uint32_t kWordOnes = 0xFFFFFFFFu;
 __device__ const uint32_t kWordZero = 0u;
 
@@ -329,9 +482,13 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     if (a.trace && tid == 0) a.trace[row * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
+  const bool rr = a.rr_eps != nullptr;
+  float eps2 = 0.f;
+  if (rr) eps2 = rr_margin(a.rr_eps[row]);
   if (tid == 0) {
     misc[7] = 0;  // candidate count
     misc[8] = 0;  // qualifying-tile count
+    misc[13] = 0;  // re-rank: rank-0 tiles
     *(uint64_t*)(misc + 10) = 0ull;  // rank-0 key of this query
   }
 
@@ -380,7 +537,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   uint32_t P0 = 0, r0_word = 0;
   int r0_tile = 0;
   float r0_val = 0.f;
-  if (prow && wave == 0) {
+  if (prow && wave == 0 && !rr) {
     uint64_t b = red[0];
 #pragma unroll
     for (int i = 1; i < kSelectThreads / 64; ++i) b = red[i] > b ? red[i] : b;
@@ -431,10 +588,12 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     T0 = ck > T0 ? ck : T0;
   }
   if (T0 == 0) T0 = 1;  // fewer than K threads see eligible items: take every eligible one
+  // re-rank: gather every item whose approximate score may still hold an exact top-K place
+  const uint32_t Tg = rr ? ord_sub(T0, eps2) : T0;
   stamp(2);
   if constexpr (ABL == 2) { if (T0 == 0x12345u) a.keys_out[row] = T0; return; }
 
-  if (prow && wave == 0) {
+  if (prow && wave == 0 && !rr) {
     uint64_t key = 0;
     if (P0) {
       // float compare: the maxima fold -0 into +0, and numpy's argmax treats them as equal
@@ -461,7 +620,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
 #pragma unroll
     for (int b = 0; b < kB; ++b) {
       const int t = tid + b * kSelectThreads;
-      qm[b] = __ballot(t < ntiles && v0[b] >= T0);
+      qm[b] = __ballot(t < ntiles && v0[b] >= Tg);
       tot += (uint32_t)__popcll(qm[b]);
     }
     if (tot) {
@@ -480,7 +639,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     }
   }
   for (int t = tid + kB * kSelectThreads; t < ntiles; t += kSelectThreads)
-    if (trow[t] >= T0) {
+    if (trow[t] >= Tg) {
       const uint32_t p = atomicAdd(&misc[8], 1u);
       if (p < (uint32_t)kTileCap) tlist[p] = (uint32_t)t;
     }
@@ -510,7 +669,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int it = 4 * c4 + c;
-        m |= (t * 32 + it < n && ((ok >> it) & 1u) && ord_of(f[c]) >= T0) ? (1u << it) : 0u;
+        m |= (t * 32 + it < n && ((ok >> it) & 1u) && ord_of(f[c]) >= Tg) ? (1u << it) : 0u;
       }
     }
     if (!m) return;
@@ -533,15 +692,108 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     // list slot i -> thread (i % 4)·64 + i / 4: a short list spreads over all four waves
     const uint32_t slot = ((uint32_t)lane << 2) | (uint32_t)wave;
     for (uint32_t i = slot; i < ntl; i += kSelectThreads) gather_tile((int)tlist[i]);
-  } else {  // list overflow (masses of ties at the bound): every tile reaching T0
+  } else {  // list overflow (masses of ties at the bound): every tile reaching the bound
     for (int t = tid; t < ntiles; t += kSelectThreads)
-      if (trow[t] >= T0) gather_tile(t);
+      if (trow[t] >= Tg) gather_tile(t);
   }
   __syncthreads();  // B4
   stamp(4);
   uint32_t cnt = misc[7];
   if constexpr (ABL == 4) { if (cnt == 0x12345u) a.keys_out[row] = cnt; return; }
-  if (cnt > (uint32_t)kCandCap) {
+  if (rr) {
+    // ---- re-rank hand-off (rerank_kernel rescores and emits).  Rank 0: the present items
+    // whose approximate score is within the margin of the approximate present maximum
+    // (typically the liked set alone) ----
+    if (prow) {
+      uint64_t b = red[0];
+#pragma unroll
+      for (int i = 1; i < kSelectThreads / 64; ++i) b = red[i] > b ? red[i] : b;
+      const uint32_t Pm = (uint32_t)(b >> 32);
+      const uint32_t thr0 = ord_sub(Pm, eps2);
+      uint32_t* r0t = (uint32_t*)(dsm + kOffR0);
+      if (Pm) {
+#pragma unroll
+        for (int bb = 0; bb < kB; ++bb) {
+          const int t = tid + bb * kSelectThreads;
+          if (t < ntiles && p0[bb] >= thr0) {
+            const uint32_t q = atomicAdd(&misc[13], 1u);
+            if (q < (uint32_t)kR0Cap) r0t[q] = (uint32_t)t;
+          }
+        }
+        for (int t = tid + kB * kSelectThreads; t < ntiles; t += kSelectThreads)
+          if (prow[t] >= thr0) {
+            const uint32_t q = atomicAdd(&misc[13], 1u);
+            if (q < (uint32_t)kR0Cap) r0t[q] = (uint32_t)t;
+          }
+      }
+      if (tid == 0) misc[14] = 0;
+      __syncthreads();
+      const uint32_t nt0 = misc[13];
+      uint32_t* r0g = a.rr_r0 + (size_t)row * kRrR0Cap;
+      if (Pm && nt0 <= (uint32_t)kR0Cap)
+        for (int i = tid; i < (int)nt0 * 32; i += kSelectThreads) {
+          const int t = (int)r0t[i >> 5], it = i & 31, j = t * 32 + it;
+          const uint32_t pw = a.present ? a.present[w0 + t] : ~0u;
+          if (j < n && ((pw >> it) & 1u) && ord_of(s_at(j)) >= thr0) {
+            const uint32_t q = atomicAdd(&misc[14], 1u);
+            if (q < (uint32_t)kRrR0Cap) r0g[q] = a.gid0 + (uint32_t)j;
+          }
+        }
+      __syncthreads();
+      if (tid == 0) {
+        a.rr_r0n[row] = !Pm ? 0u : (nt0 > (uint32_t)kR0Cap || misc[14] > (uint32_t)kRrR0Cap) ? kRrSlow : misc[14];
+        a.rr_thr[2 * row + 1] = thr0;
+      }
+    }
+    if (cnt > (uint32_t)kCandCap) {  // masses of items at the bound: the exact slow path
+      if (tid == 0) {
+        a.rr_cnt[row] = kRrSlow;
+        a.rr_thr[2 * row] = Tg;
+      }
+      return;
+    }
+    // ---- approximate order -> the K-th approximate score -> the candidates within 2ε ----
+    if (cnt <= 256) {
+      if (wave == 0) {
+        uint64_t v[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) v[s4] = s4 * 64 + lane < (int)cnt ? cand[s4 * 64 + lane] : 0ull;
+        wave_bitonic_desc<4>(v, lane);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          if (s4 * 64 + lane < (int)cnt) cand[s4 * 64 + lane] = v[s4];
+      }
+      __syncthreads();
+    } else {
+      int P = 1;
+      while (P < (int)cnt) P <<= 1;
+      for (int i = (int)cnt + tid; i < P; i += kSelectThreads) cand[i] = 0ull;
+      __syncthreads();
+      bitonic_desc_u64(cand, P);
+    }
+    uint32_t m = cnt;
+    if (cnt >= (uint32_t)K) {
+      const uint32_t thr = ord_sub(ordk_of(cand[K - 1]), eps2);
+      // sorted: the prefix of keys reaching thr (thread-parallel boundary search)
+      if (tid == 0) misc[12] = cnt;
+      __syncthreads();
+      for (int i = tid; i < (int)cnt; i += kSelectThreads)
+        if (ordk_of(cand[i]) >= thr && (i + 1 == (int)cnt || ordk_of(cand[i + 1]) < thr)) misc[12] = (uint32_t)(i + 1);
+      __syncthreads();
+      m = misc[12];
+    }
+    if (m > (uint32_t)kRrCap) {
+      if (tid == 0) {
+        a.rr_cnt[row] = kRrSlow;
+        a.rr_thr[2 * row] = Tg;
+      }
+      return;
+    }
+    uint64_t* out = a.rr_out + (size_t)row * kRrCap;
+    for (int i = tid; i < (int)m; i += kSelectThreads) out[i] = cand[i];
+    if (tid == 0) a.rr_cnt[row] = m;
+    return;
+  } else if (cnt > (uint32_t)kCandCap) {
     __syncthreads();
     auto ord_at = [&](int j) -> uint32_t {
       const uint32_t ok = elig(j >> 5);
@@ -552,11 +804,12 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   const uint64_t gmax = *(const uint64_t*)(misc + 10);  // 0 = no rank-0 drop
 
   // ---- sort candidates by full key, emit the top K ----
-  if (cnt <= 256) {  // one wave, registers only
+  if (cnt <= 256 || (rr && cnt <= 512)) {  // one wave, registers only
     if (wave != 0) return;
     if (cnt <= 64) wave_sort_emit<1>(cand, (int)cnt, a, row, gmax);
     else if (cnt <= 128) wave_sort_emit<2>(cand, (int)cnt, a, row, gmax);
-    else wave_sort_emit<4>(cand, (int)cnt, a, row, gmax);
+    else if (cnt <= 256) wave_sort_emit<4>(cand, (int)cnt, a, row, gmax);
+    else wave_sort_emit<8>(cand, (int)cnt, a, row, gmax);
     if (a.trace && tid == 0) {
       stamp(5);
       a.trace[row * 8 + 6] = cnt;
@@ -786,6 +1039,102 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
   else if (m <= 128) wave_sort_emit<2>(sel, m, sa, row, drop);
   else if (m <= 256) wave_sort_emit<4>(sel, m, sa, row, drop);
   else wave_sort_emit<8>(sel, m, sa, row, drop);
+}
+
+// ---- exact re-rank, second stage (SelectArgs.rr_*) ------------------------------------------
+// One workgroup per query: the exact rank 0 from its approximate candidates, then the
+// candidates within 2ε of the K-th approximate score rescored from the f32 rows (16-lane
+// groups, four rows in flight per group), sorted by the exact key and emitted as the final
+// list (rank 0 dropped when it heads it) or the key list.  Rows the select flagged kRrSlow
+// (masses of items at the bound) take the exact running top-K over the whole row.
+constexpr int kRrOffQ = 2560 * 8;
+constexpr int kRrOffMisc = kRrOffQ + kRrMaxD * 4;
+constexpr int kRrLds = kRrOffMisc + 256;
+
+__global__ __launch_bounds__(kSelectThreads) void rerank_kernel(SelectArgs a) {
+  __shared__ __attribute__((aligned(16))) char dsm[kRrLds];
+  uint64_t* cand = (uint64_t*)dsm;
+  float* qs = (float*)(dsm + kRrOffQ);
+  uint32_t* misc = (uint32_t*)(dsm + kRrOffMisc);
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = a.n_cols, K = a.K;
+  const int ntiles = (n + 31) >> 5;
+  const float* Srow = a.S + (size_t)row * a.lds;
+  auto s_at = [&](int j) -> float {
+    return a.s_blocked ? a.S[sblk_quad(row, j >> 5, (j >> 2) & 7, a.ldt) + (j & 3)] : Srow[j];
+  };
+  const uint32_t* excl = a.excl ? a.excl + (size_t)row * a.excl_ld : nullptr;
+  const int64_t w0 = a.slab_start >> 5;
+  auto elig = [&](int tile) -> uint32_t {
+    const uint32_t* pp = a.present ? a.present + w0 + tile : &kWordOnes;
+    const uint32_t* mp = a.mask ? a.mask + w0 + tile : &kWordOnes;
+    const uint32_t* ep = excl ? excl + w0 + tile : &kWordZero;
+    return *pp & *mp & ~*ep;
+  };
+  const uint32_t m = a.rr_cnt[row];
+  const uint64_t* src = a.rr_out + (size_t)row * kRrCap;
+  const float4* qg = (const float4*)(a.rr_q + (size_t)row * a.rr_ld);
+  for (int i = tid; i < (a.rr_d >> 2); i += kSelectThreads) ((float4*)qs)[i] = qg[i];
+  if (m != kRrSlow)
+    for (int i = tid; i < (int)m; i += kSelectThreads) cand[i] = src[i];
+  uint32_t n0 = 0;
+  if (a.max_inout) {
+    n0 = a.rr_r0n[row];
+    if (n0 != kRrSlow)
+      for (int i = tid; i < (int)n0; i += kSelectThreads) cand[2048 + i] = make_key(1u, a.rr_r0[(size_t)row * kRrR0Cap + i]);
+  }
+  if (tid == 0) *(uint64_t*)(misc + 10) = 0ull;
+  __syncthreads();
+  // ---- exact rank 0 ----
+  if (a.max_inout) {
+    uint64_t best0 = 0;
+    if (n0 != kRrSlow) {
+      rr_rescore_any(cand + 2048, (int)n0, a, qs);
+      __syncthreads();
+      for (int i = tid; i < (int)n0; i += kSelectThreads) best0 = cand[2048 + i] > best0 ? cand[2048 + i] : best0;
+    } else {  // masses of near-duplicates at the top: every present item within the margin
+      const uint32_t thr0 = a.rr_thr[2 * row + 1];
+      const uint32_t* prow = a.pmax + (size_t)row * a.ldt;
+      for (int i = tid; i < ntiles * 32; i += kSelectThreads) {
+        const int t = i >> 5, it = i & 31;
+        if (prow[t] < thr0) continue;
+        const uint32_t pw = a.present ? a.present[w0 + t] : ~0u;
+        if (i < n && ((pw >> it) & 1u) && ord_of(s_at(i)) >= thr0) {
+          const uint32_t gid = a.gid0 + (uint32_t)i;
+          const uint64_t k = rr_key(rr_dot_thread(a.rr_x + (size_t)(gid - a.rr_gid_base) * a.rr_ld, qs, a.rr_d >> 2), gid);
+          best0 = k > best0 ? k : best0;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t y = __shfl_xor(best0, o);
+      best0 = y > best0 ? y : best0;
+    }
+    if (lane == 0) atomicMax((unsigned long long*)(misc + 10), (unsigned long long)best0);
+    __syncthreads();
+    if (tid == 0) a.max_inout[row] = *(const uint64_t*)(misc + 10);
+  }
+  if (m == kRrSlow) {
+    rr_slow_path(a, row, n, a.rr_thr[2 * row], K, cand, misc, qs, elig, s_at);
+    return;
+  }
+  rr_rescore_any(cand, (int)m, a, qs);
+  __syncthreads();
+  const uint64_t gmax = *(const uint64_t*)(misc + 10);
+  if (wave != 0) return;
+  if (m <= 64) wave_sort_emit<1>(cand, (int)m, a, row, gmax);
+  else if (m <= 128) wave_sort_emit<2>(cand, (int)m, a, row, gmax);
+  else if (m <= 256) wave_sort_emit<4>(cand, (int)m, a, row, gmax);
+  else wave_sort_emit<8>(cand, (int)m, a, row, gmax);
+}
+
+hipError_t launch_rerank(const SelectArgs& a, int B, hipStream_t s) {
+  if (!a.rr_eps || !a.rr_x || !a.rr_q || !a.rr_out || !a.rr_cnt || !a.rr_thr || (a.max_inout && (!a.rr_r0 || !a.rr_r0n)) ||
+      a.rr_d <= 0 || a.rr_d > kRrMaxD || (a.rr_d & 3) || a.K <= 0 || a.K > kMaxKInt || B <= 0)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rerank_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s) {

@@ -1,0 +1,143 @@
+"""GPU parity of the exact re-rank path of an f32 index (one slab): a one-product bf16 MFMA
+scan gives approximate scores within a proven bound ε of the exact ones, and the select
+rescores every candidate within 2ε of the K-th from the f32 rows (f64 sum, rounded to f32).
+
+The re-ranked lists are therefore checked BIT-EXACTLY (ids in order and score bits) against
+an f64 recompute over the device's own f32 operands — the stored normalised rows
+(bb_get_rows) and the query normalised like prep (f64 norm, f32 quotient) — ranked by
+(f32 score desc, id asc).  Cases: the configs[1] shape, masses of near-duplicate rows
+(more than 2048 candidates within the margin: the slow path), near-duplicate rank 0
+(similar-sets), hybrid CF side, and masks.
+"""
+import numpy as np
+import pytest
+
+from oracle import restatement as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def brickrec():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+    import brickrec as br
+    return br
+
+
+def _qop(q):
+    q64 = q.astype(np.float64)
+    n = np.sqrt((q64 * q64).sum(1, keepdims=True))
+    n[n == 0] = 1.0
+    return (q64 / n).astype(np.float32)
+
+
+def _exact_topk(rows32, q32, k, allowed=None, drop_rank0_present=None):
+    """f32(f64 dot) scores over the device operands; top-k by (score desc, id asc)."""
+    s = (rows32.astype(np.float64) @ q32.astype(np.float64)).astype(np.float32)
+    ok = np.ones(len(s), bool) if allowed is None else allowed.copy()
+    if drop_rank0_present is not None:
+        p = np.where(drop_rank0_present, s, -np.inf)
+        m = p.max()
+        r0 = int(np.flatnonzero(p == m)[0])
+        ok[r0] = False
+    idx = np.flatnonzero(ok)
+    o = np.lexsort((idx, -s[idx]))[:k]
+    return idx[o], s[idx[o]]
+
+
+def _assert_exact(sc, ids, ri, rs):
+    L = len(ri)
+    assert list(ids[:L]) == list(ri), (ids[:L], ri)
+    assert np.array_equal(sc[:L].view(np.uint32), rs.astype(np.float32).view(np.uint32))
+
+
+def test_rr_configs1_shape_bit_exact(brickrec):
+    n, d, B, k = 25216, 384, 256, 50
+    x = R.unit_rows(n, d, 1234)
+    q = R.unit_rows(B, d, 4321)
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(x)
+    idx.set_profiling(True)
+    sc, ids, cnt = idx.search("semantic", k, q_rows=q)
+    prof = idx.profile()
+    assert prof["gemm"]["launches"] == 1 and prof["select"]["launches"] == 1, prof
+    rows = idx.get_rows(np.arange(n))
+    qo = _qop(q)
+    for i in range(0, B, 4):
+        ri, rs = _exact_topk(rows, qo[i], k)
+        _assert_exact(sc[i], ids[i], ri, rs)
+
+
+def test_rr_near_duplicates_slow_path(brickrec):
+    """3,000 rows within ~1e-4 of the query direction: every one of them is inside the
+    approximate scan's margin, so the select takes the exact running top-K path."""
+    rng = np.random.default_rng(8)
+    n, d, k = 20000, 384, 50
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    v = rng.standard_normal(d).astype(np.float32)
+    dup = rng.choice(n, 3000, replace=False)
+    x[dup] = v + 3e-3 * rng.standard_normal((3000, d)).astype(np.float32)
+    mask = rng.random(n) < 0.7
+    q = np.stack([v, x[dup[0]], rng.standard_normal(d).astype(np.float32)])
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(x)
+    rows = idx.get_rows(np.arange(n))
+    qo = _qop(q)
+    for m in (None, mask):
+        sc, ids, cnt = idx.search("semantic", k, q_rows=q, mask=m)
+        for i in range(len(q)):
+            ri, rs = _exact_topk(rows, qo[i], k, m)
+            _assert_exact(sc[i], ids[i], ri, rs)
+    # similar-sets from inside the cluster: rank 0 (the item itself) among thousands of
+    # near-duplicates; drop it, then the exact masked top-k
+    qi = dup[:6]
+    sc, ids, cnt = idx.search("similar", k, q_items=qi, mask=mask)
+    for j, it in enumerate(qi):
+        ri, rs = _exact_topk(rows, rows[it], k, mask, drop_rank0_present=np.ones(n, bool))
+        _assert_exact(sc[j], ids[j], ri, rs)
+
+
+def test_rr_exact_duplicate_rank0(brickrec):
+    """Exact duplicates of the liked set: rank 0 is the lowest id of the tied maxima (numpy
+    argmax / the fixed tie rule); the duplicate then heads the list."""
+    rng = np.random.default_rng(9)
+    n, d, k = 5000, 128, 20
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    x[[100, 2000, 4000]] = x[3000]
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(x)
+    rows = idx.get_rows(np.arange(n))
+    sc, ids, cnt = idx.search("similar", k, q_items=[3000, 100])
+    for j, it in enumerate((3000, 100)):
+        ri, rs = _exact_topk(rows, rows[it], k, drop_rank0_present=np.ones(n, bool))
+        _assert_exact(sc[j], ids[j], ri, rs)
+        assert ri[0] in (100, 2000, 3000, 4000) and 100 not in list(ri)
+
+
+def test_rr_cf_and_hybrid_sides_exact(brickrec):
+    """CF factors (not normalised, r=50): the CF side's keys are exact as well."""
+    rng = np.random.default_rng(10)
+    n, d, r, B, k = 30000, 384, 50, 64, 25
+    x = R.unit_rows(n, d, 11)
+    f = rng.normal(0, 0.1, (n, r)).astype(np.float32)
+    u = rng.normal(0, 0.1, (B, r)).astype(np.float32)
+    excl = rng.random((B, n)) < 0.01
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(x)
+    idx.upload_cf(f)
+    sc, ids, cnt = idx.search("cf", k, q_cf=u, excl=excl)
+    for i in range(0, B, 3):
+        ri, rs = _exact_topk(f, u[i], k, ~excl[i])
+        _assert_exact(sc[i], ids[i], ri, rs)
+    # hybrid: the device union blend of the two exact side lists
+    qi = rng.choice(n, B, replace=False)
+    hs, hid, hc = idx.search("hybrid", k, q_items=qi, q_cf=u, excl=excl)
+    rows = idx.get_rows(np.arange(n))
+    for i in range(0, B, 5):
+        ci, cs = _exact_topk(rows, rows[qi[i]], 2 * k, drop_rank0_present=np.ones(n, bool))
+        fi, fs = _exact_topk(f, u[i], 2 * k, ~excl[i])
+        bi, bs = R.union_blend(ci, cs.astype(np.float64), fi, fs.astype(np.float64), 0.4, 0.6, k)
+        assert list(hid[i][: len(bi)]) == list(bi)
+        np.testing.assert_allclose(hs[i][: len(bi)], bs, atol=1e-6, rtol=0)

@@ -43,9 +43,25 @@ def _both(idx, mode, k, stream_gemms=None, **kw):
     return a, b
 
 
-def _same(a, b):
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y)
+def _same(a, b, exact=True):
+    """Stream vs slab results.  A bf16 index runs the same scan kernels on both paths, so the
+    lists are bitwise equal.  An f32 index streams through the split-precision scan (fp32-
+    class, |error| ~1e-7) while its one-slab search runs the exact re-rank, so there the
+    scores agree within 1e-6 and the ids wherever adjacent scores are further apart."""
+    if exact:
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+        return
+    (sa, ia, ca), (sb, ib, cb) = a, b
+    assert np.array_equal(ca, cb)
+    np.testing.assert_allclose(sa, sb, atol=1e-6, rtol=0)
+    for i in range(len(ca)):
+        c = int(ca[i])
+        if c > 1 and np.all(-np.diff(sb[i][:c].astype(np.float64)) > 2e-6):
+            assert list(ia[i][:c]) == list(ib[i][:c]), i
+        elif c:
+            sure = set(ib[i][:c][sb[i][:c] > sb[i][c - 1] + 2e-6])
+            assert sure <= set(ia[i][:c]), i
 
 
 def test_stream_semantic_f32_vs_oracle(brickrec):
@@ -55,7 +71,7 @@ def test_stream_semantic_f32_vs_oracle(brickrec):
     idx = brickrec.ItemIndex(dtype="f32")
     idx.upload_items(x)
     (sc, ids, cnt), slab = _both(idx, "semantic", k, stream_gemms=2, q_rows=q)
-    _same((sc, ids, cnt), slab)
+    _same((sc, ids, cnt), slab, exact=False)
     assert np.all(cnt == k)
     sim = R.cosine_scores(q, x).astype(np.float64)
     gate = Gate("stream f32 150K x 384 semantic top-100")
@@ -109,10 +125,10 @@ def test_stream_hybrid_cf_excl(brickrec):
     idx.upload_items(x)
     idx.upload_cf(f)
     a, b = _both(idx, "hybrid", k, stream_gemms=4, q_items=qi, q_cf=u, mask=mask, excl=excl)
-    _same(a, b)
+    _same(a, b, exact=False)
     hyb = a
     a, b = _both(idx, "cf", k, stream_gemms=2, q_cf=u, mask=mask, excl=excl)
-    _same(a, b)
+    _same(a, b, exact=False)
     sc, ids, cnt = a
     for i in range(0, B, 7):
         ri, rs = R.cf_topk(u[i], f, k, mask & ~excl[i])
@@ -146,7 +162,7 @@ def test_stream_two_query_chunks(brickrec):
     # a 16 MiB workspace cannot hold 1100 pilot rows: query chunks of 512, 512 and 76 (ragged)
     idx.set_option("workspace_bytes", 16 << 20)
     (sc, ids, cnt), slab = _both(idx, "semantic", k, stream_gemms=6, q_rows=q)
-    _same((sc, ids, cnt), slab)
+    _same((sc, ids, cnt), slab, exact=False)
     sim = R.cosine_scores(q[-5:], x).astype(np.float64)
     for j in range(5):
         ri, rs = R.topk_indices(sim[j], k)
@@ -178,7 +194,7 @@ def test_stream_small_index_forced(brickrec):
     idx.upload_items(x)
     qi = np.arange(B) * 7
     a, b = _both(idx, "similar", k, stream_gemms=2, q_items=qi)
-    _same(a, b)
+    _same(a, b, exact=False)
     for i in range(0, B, 9):
         ri, rs = R.similar_sets(x, int(qi[i]), k)
         assert list(a[1][i]) == list(ri)
@@ -252,7 +268,7 @@ def test_stream_two_level_bound(brickrec, dtype, mode):
     assert prof["select"]["launches"] == 3, prof   # pilot slab, pass A list, final
     idx.set_option("stream", 0)
     b = idx.search(mode, k, **kw)
-    _same(a, b)
+    _same(a, b, exact=dtype == "bf16")
     assert np.all(a[2] == k)
     if mode == "similar":
         for i in range(B):

@@ -39,6 +39,11 @@ CASES = {
     "c5-full": dict(n=10000000, d=384, B=8192, k=100, dtype="bf16", mode="semantic"),
     # an f32 index at scale (MiniLM embeddings are f32): the split-precision streaming scan
     "f32-1M": dict(n=1000000, d=384, B=4096, k=100, dtype="f32", mode="semantic"),
+    # bf16 index at the 25K shape (the one-product MFMA scan, no split)
+    "b2-B1": dict(n=25216, d=384, B=1, k=50, dtype="bf16", mode="semantic"),
+    "b2-B256": dict(n=25216, d=384, B=256, k=50, dtype="bf16", mode="semantic"),
+    "b2-B1024": dict(n=25216, d=384, B=1024, k=50, dtype="bf16", mode="semantic"),
+    "b2-B4096": dict(n=25216, d=384, B=4096, k=50, dtype="bf16", mode="semantic"),
     # north_star latency points: small batches against the large indexes
     "c4-B1": dict(n=1000000, d=768, B=1, k=100, dtype="bf16", mode="semantic"),
     "c4-B256": dict(n=1000000, d=768, B=256, k=100, dtype="bf16", mode="semantic"),
