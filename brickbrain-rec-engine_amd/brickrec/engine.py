@@ -334,6 +334,45 @@ class ItemIndex:
                                           int(n_parts), C.byref(res)), "bb_finalize")
         return out
 
+    def search_hybrid_sides(self, k: int, *, q_items, q_cf, mask=None, excl=None, k_side: int = 0,
+                            w_content: float = 0.4, w_cf: float = 0.6):
+        """HYBRID in one device pass with each final item's side membership: bb_search (both
+        sides scored and selected in the same search, key lists out) then bb_finalize (rank-0
+        drop, union blend wc·c + wcf·cf in f64 on the device).  Host inputs; returns numpy
+        (scores [B,k], ids [B,k], counts [B], in_content [B,k] bool, in_cf [B,k] bool, side
+        lists [B] of (content ids, CF ids)).  The membership is what
+        _combine_recommendations (recommendation_system.py:789-843) builds its reasons from."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        qi = torch.as_tensor(np.ascontiguousarray(np.asarray(q_items, np.int64))).to(dev)
+        qc_np = np.ascontiguousarray(q_cf if np.asarray(q_cf).dtype in (np.float32, np.float64)
+                                     else np.asarray(q_cf, np.float64))
+        qc = torch.as_tensor(qc_np).to(dev)
+        words = lambda m: None if m is None else torch.as_tensor(
+            (np.asarray(m, np.uint32) if np.asarray(m).dtype == np.uint32 else bits_from_bool(m)).view(np.int32)).to(dev)
+        keys, maxk = self.search_keys("hybrid", k, q_items=qi, q_cf=qc, mask=words(mask), excl=words(excl),
+                                      k_side=k_side)
+        sc, ids, cnt = self.finalize("hybrid", k, keys[None], maxk[None], 1, k_side=k_side, w_content=w_content,
+                                     w_cf=w_cf)
+        sc, ids, cnt = sc.cpu().numpy(), ids.cpu().numpy(), cnt.cpu().numpy()
+        kk = keys.cpu().numpy().view(np.uint64)
+        mk = maxk.cpu().numpy().view(np.uint64)
+        ks = k_side or 2 * k
+        gid = lambda u: (np.uint64(0xFFFFFFFF) - (u & np.uint64(0xFFFFFFFF))).astype(np.int64)
+        in_c = np.zeros(ids.shape, bool)
+        in_f = np.zeros(ids.shape, bool)
+        sides = []
+        for b in range(ids.shape[0]):
+            c = kk[0, b][kk[0, b] != 0]
+            if len(c) and mk[b] and c[0] == mk[b]:   # the rank-0 drop finalize applies
+                c = c[1:]
+            f = kk[1, b][kk[1, b] != 0]
+            cs, fs = set(gid(c[:ks]).tolist()), gid(f[:ks])
+            in_c[b] = [int(i) in cs for i in ids[b]]
+            in_f[b] = np.isin(ids[b], fs)
+            sides.append((gid(c[:ks]), fs))
+        return sc, ids, cnt, in_c & (ids >= 0), in_f & (ids >= 0), sides
+
     def get_rows(self, ids):
         """Stored (normalised) rows of global ids: numpy in -> numpy out (f32 view of the
         index dtype: f32, or bf16 widened), torch CUDA int64 in -> torch tensor out."""

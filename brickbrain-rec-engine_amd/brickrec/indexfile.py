@@ -11,11 +11,14 @@ staging chunks, with no Python-side copy.
 
 Layout (little endian; every section 4-KiB aligned)::
 
-    0   magic "BBIX", u32 version (1), u64 n, u32 d, u32 flags (bit 0: rows unit-norm),
-        u64 off_rows, u64 off_attrs, u64 off_names, u64 names_bytes
+    0   magic "BBIX", u32 version (2; 1 is read too), u64 n, u32 d, u32 flags (bit 0: rows
+        unit-norm, bit 1: attributes, bit 2: documents), u64 off_rows, u64 off_attrs,
+        u64 off_names, u64 names_bytes, [v2] u64 off_docs, u64 docs_bytes
     off_rows   f32 [n][d]                      item rows (row i = global id i)
     off_attrs  i32 num_parts[n], i16 year[n], i32 theme_id[n]   (bb_upload_attrs columns)
     off_names  UTF-8 JSON list of set_num strings (row order)
+    off_docs   UTF-8 JSON {"descriptions": [n], "metadata": [n]} — the document each row
+               embeds (brickrec/documents.py: prep_vectorDB's text, in its row order)
 
 Data only: nothing in the file is executed, and readers check every offset against the
 file size.
@@ -30,8 +33,9 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 MAGIC = b"BBIX"
-VERSION = 1
-_HDR = struct.Struct("<4sIQIIQQQQ")
+VERSION = 2
+_HDR = struct.Struct("<4sIQIIQQQQ")     # v1 header
+_HDR2 = struct.Struct("<QQ")            # v2 extension: off_docs, docs_bytes
 _ALIGN = 4096
 
 
@@ -40,20 +44,30 @@ def _align(x: int) -> int:
 
 
 def write_index(path: str, set_nums: Sequence[str], rows: np.ndarray, num_parts=None, year=None, theme_id=None,
-                unit_norm: bool = False) -> None:
-    """Write rows (n×d, stored as f32) and the optional attribute columns."""
+                unit_norm: bool = False, documents=None) -> None:
+    """Write rows (n×d, stored as f32), the optional attribute columns, and optionally the
+    documents the rows embed: (descriptions, metadata) lists in row order, e.g. from
+    documents.build_documents."""
     rows = np.asarray(rows)
     n, d = rows.shape
     if len(set_nums) != n:
         raise ValueError("one set_num per row")
     names = json.dumps([str(s) for s in set_nums]).encode()
-    off_rows = _align(_HDR.size)
+    docs = b""
+    if documents is not None:
+        desc, meta = documents
+        if len(desc) != n or len(meta) != n:
+            raise ValueError("one document per row")
+        docs = json.dumps({"descriptions": list(desc), "metadata": list(meta)}).encode()
+    off_rows = _align(_HDR.size + _HDR2.size)
     off_attrs = _align(off_rows + n * d * 4)
     has_attrs = num_parts is not None
     off_names = _align(off_attrs + (n * 10 if has_attrs else 0))
-    flags = (1 if unit_norm else 0) | (2 if has_attrs else 0)
+    off_docs = _align(off_names + len(names))
+    flags = (1 if unit_norm else 0) | (2 if has_attrs else 0) | (4 if docs else 0)
     with open(path, "wb") as f:
         f.write(_HDR.pack(MAGIC, VERSION, n, d, flags, off_rows, off_attrs, off_names, len(names)))
+        f.write(_HDR2.pack(off_docs if docs else 0, len(docs)))
         f.seek(off_rows)
         for i in range(0, n, 1 << 16):  # bounded host memory for large matrices
             f.write(np.ascontiguousarray(rows[i:i + (1 << 16)], dtype=np.float32).tobytes())
@@ -64,6 +78,9 @@ def write_index(path: str, set_nums: Sequence[str], rows: np.ndarray, num_parts=
             f.write(np.ascontiguousarray(theme_id, np.int32).tobytes())
         f.seek(off_names)
         f.write(names)
+        if docs:
+            f.seek(off_docs)
+            f.write(docs)
 
 
 class IndexFile:
@@ -73,15 +90,20 @@ class IndexFile:
     def __init__(self, path: str):
         size = os.path.getsize(path)
         with open(path, "rb") as f:
-            hdr = f.read(_HDR.size)
+            hdr = f.read(_HDR.size + _HDR2.size)
         if len(hdr) < _HDR.size:
             raise ValueError(f"{path}: truncated header")
-        magic, ver, n, d, flags, off_rows, off_attrs, off_names, names_bytes = _HDR.unpack(hdr)
-        if magic != MAGIC or ver != VERSION:
-            raise ValueError(f"{path}: not a brickrec index file (v{VERSION})")
+        magic, ver, n, d, flags, off_rows, off_attrs, off_names, names_bytes = _HDR.unpack(hdr[:_HDR.size])
+        if magic != MAGIC or ver not in (1, 2):
+            raise ValueError(f"{path}: not a brickrec index file (v1 / v2)")
+        off_docs = docs_bytes = 0
+        if ver >= 2:
+            if len(hdr) < _HDR.size + _HDR2.size:
+                raise ValueError(f"{path}: truncated header")
+            off_docs, docs_bytes = _HDR2.unpack(hdr[_HDR.size:])
         has_attrs = bool(flags & 2)
         if (off_rows + n * d * 4 > size or (has_attrs and off_attrs + n * 10 > size)
-                or off_names + names_bytes > size):
+                or off_names + names_bytes > size or (flags & 4 and off_docs + docs_bytes > size)):
             raise ValueError(f"{path}: sections past the end of the file")
         self.path, self.n, self.d = path, int(n), int(d)
         self.unit_norm = bool(flags & 1)
@@ -97,6 +119,14 @@ class IndexFile:
             self.set_nums: List[str] = json.loads(f.read(names_bytes).decode())
         if len(self.set_nums) != self.n:
             raise ValueError(f"{path}: {len(self.set_nums)} names for {self.n} rows")
+        self.descriptions = self.metadata = None
+        if flags & 4:
+            with open(path, "rb") as f:
+                f.seek(off_docs)
+                dd = json.loads(f.read(docs_bytes).decode())
+            self.descriptions, self.metadata = dd["descriptions"], dd["metadata"]
+            if len(self.descriptions) != self.n or len(self.metadata) != self.n:
+                raise ValueError(f"{path}: document count does not match the rows")
 
     def load_into(self, index, present: Optional[np.ndarray] = None):
         """Upload the rows (and attributes) into an ``ItemIndex`` straight from the mapping."""

@@ -463,6 +463,12 @@ class HybridRecommender:
             mask = constraint_result.valid_mask
         content_recs: List[RecommendationResult] = []
         collaborative_recs: List[RecommendationResult] = []
+        fused = self._device_hybrid(user_id, liked_set, top_k, self._mask_for(mask))
+        if fused is not None:
+            if constraint_result and constraint_result.violations:
+                for rec in fused:
+                    rec.constraint_violations = [v.message for v in constraint_result.violations]
+            return fused, constraint_result
         if liked_set:
             cr = self.content_recommender
             if cr.feat_matrix is None:
@@ -492,6 +498,58 @@ class HybridRecommender:
             for rec in final:
                 rec.constraint_violations = [v.message for v in constraint_result.violations]
         return final, constraint_result
+
+    def _device_hybrid(self, user_id, liked_set, top_k: int, mask: Optional[np.ndarray]
+                       ) -> Optional[List[RecommendationResult]]:
+        """Both sides available (a known liked set and a user the CF model knows): the whole
+        hybrid — content top-2k, CF top-2k, union blend (:646-668, :789-843) — in ONE device
+        HYBRID search (bb_search + bb_finalize); reasons follow each item's side membership
+        as in _combine_recommendations.  None = take the per-side path (a side is missing,
+        a cold-start user, or a CF-side set without a catalogue row, which the reference's
+        _get_set_details would drop, :470-471)."""
+        if not liked_set or not user_id or top_k <= 0:
+            return None
+        cr, cf = self.content_recommender, self.collaborative_recommender
+        if cr.feat_matrix is None:
+            cr.prepare_features()
+        if liked_set not in cr._row_of_set:
+            return None
+        if cf.svd_model is None:
+            cf.train_svd_model()
+        u = cf._lookup(user_id) if cf.svd_model is not None else None
+        if u is None:
+            return None
+        cat = self.engine.catalog
+        idx = self.engine.ensure_index()
+        sc, ids, cnt, in_c, in_f, sides = idx.search_hybrid_sides(
+            top_k, q_items=[cat.pos[liked_set]], q_cf=cf.user_factors[[u]], excl=cf.rated_mask(u)[None, :],
+            mask=mask, w_content=self.content_weight, w_cf=self.collaborative_weight)
+        c_ids, f_ids = sides[0]
+        if len(f_ids) and int(np.max(f_ids)) >= cat.n_db:
+            return None
+        if len(c_ids) == 0 or len(f_ids) == 0:
+            # one side produced nothing: the reference then takes the other side's top k with
+            # its own scores (:659-662), which the per-side path reproduces
+            return None
+        t = cr._row_of_set[liked_set]
+        out = []
+        for j in range(int(cnt[0])):
+            g = int(ids[0][j])
+            reasons = []
+            if in_c[0][j]:
+                i = int(cr._content_row[g])
+                reasons += [f"Content: {x}" for x in cr._generate_content_reasons_rows(i, t)]
+                base = dict(set_num=cr.set_lookup[i], name=cr.set_feat["name"].iat[i],
+                            theme_name=cr._r_theme_name[i], year=int(cr._r_year[i]),
+                            num_parts=int(cr.set_feat["num_parts"].iat[i]), img_url=cr.set_feat["img_url"].iat[i])
+            else:
+                d = cat.details(g)
+                base = dict(set_num=d["set_num"], name=d["name"], theme_name=d["theme_name"], year=d["year"],
+                            num_parts=d["num_parts"], img_url=d["img_url"])
+            if in_f[0][j]:
+                reasons.append("Community: Users with similar preferences also liked this set")
+            out.append(RecommendationResult(score=float(sc[0][j]), reasons=reasons, **base))
+        return out
 
     def _mask_for(self, mask: Optional[np.ndarray]) -> Optional[np.ndarray]:
         """Pad a constraint mask to the current catalogue size (rows appended since)."""

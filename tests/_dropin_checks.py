@@ -119,3 +119,17 @@ def check_hybrid(hy, golden):
         L = int(g4["lens"][case])
         _eq_lists([pos[r.set_num] for r in recs], [r.score for r in recs], g4["ids"][case][:L],
                   g4["scores"][case][:L])
+        if u >= 0 and qrow >= 0:
+            # the one-pass device HYBRID path must build the same records as the per-side
+            # lists + _combine_recommendations (recommendation_system.py:789-843)
+            cf = hy.collaborative_recommender
+            m = hy._mask_for(res.valid_mask) if res is not None else None
+            c = hy.content_recommender.similar_by_mask(rows[int(qrow)], 2 * k, m)
+            f = cf.recommend_by_mask(cf._lookup(int(u)), 2 * k, m)
+            if c and f:
+                want = hy._combine_recommendations(c, f, k)
+                assert [r.set_num for r in recs] == [r.set_num for r in want]
+                assert [r.reasons for r in recs] == [r.reasons for r in want]
+                assert [(r.name, r.year, r.num_parts, r.theme_name) for r in recs] == \
+                    [(r.name, r.year, r.num_parts, r.theme_name) for r in want]
+                np.testing.assert_allclose([r.score for r in recs], [r.score for r in want], atol=1e-6)

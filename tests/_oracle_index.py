@@ -90,3 +90,23 @@ class OracleIndex:
             sc[b, :n] = s
             cnt[b] = n
         return sc, ids, cnt
+
+    def search_hybrid_sides(self, k, *, q_items, q_cf, mask=None, excl=None, k_side=0, w_content=0.4, w_cf=0.6):
+        B = len(q_items)
+        ks = k_side or 2 * k
+        sc = np.zeros((B, k), np.float32)
+        ids = np.full((B, k), -1, np.int64)
+        cnt = np.zeros(B, np.int32)
+        in_c = np.zeros((B, k), bool)
+        in_f = np.zeros((B, k), bool)
+        sides = []
+        for b in range(B):
+            ci, cs = self._content(int(q_items[b]), ks, mask)
+            fi, fs = self._cf(q_cf[b], ks, mask, None if excl is None else excl[b])
+            i, s = R.union_blend(ci, cs, fi, fs, w_content, w_cf, k)
+            n = len(i)
+            ids[b, :n], sc[b, :n], cnt[b] = i, s, n
+            in_c[b, :n] = np.isin(i, ci)
+            in_f[b, :n] = np.isin(i, fi)
+            sides.append((np.asarray(ci, np.int64), np.asarray(fi, np.int64)))
+        return sc, ids, cnt, in_c, in_f, sides
