@@ -109,6 +109,8 @@ struct bb_index {
   DevBuf rr_out, rr_cnt, rr_thr, rr_r0, rr_r0n;  // re-rank: select -> rerank hand-off
   // streaming top-K (large indexes): pilot lists, candidate regions, overflow flag
   DevBuf pilot, cand, cand_cnt, cand_pmax, ovf;
+  DevBuf trace;        // BB_SELECT_TRACE probe stamps
+  DevBuf rr_flags;     // one-wave re-rank select: rows left to the block select
   DevBuf list1, max1;  // two-level streaming: exact top-K_int (+ rank-0 key) of items [0, n1)
   uint32_t* ovf_host = nullptr;  // pinned
 
@@ -269,7 +271,7 @@ int bb_destroy(bb_index* x) {
                       &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
                       &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
                       &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->rr_out, &x->rr_cnt,
-                      &x->rr_thr, &x->rr_r0, &x->rr_r0n})
+                      &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
     if (x->has_last) (void)hipEventSynchronize(x->done);
@@ -610,7 +612,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   if (need_cf && (rc = x->qcf.ensure(std::max((size_t)Bc * x->Rpad * qes_f, (size_t)Bc * x->Rpad_b * 2)))) return rc;
   if (rr_c && ((rc = x->qf32.ensure((size_t)Bc * x->Dpad * 4)) || (rc = x->qeps.ensure((size_t)Bc * 4)))) return rc;
   if (rr_f && ((rc = x->qcf32.ensure((size_t)Bc * x->Rpad * 4)) || (rc = x->qcfeps.ensure((size_t)Bc * 4)))) return rc;
-  if ((rr_c || rr_f) &&
+  // the select kernel rescores its candidates itself; BB_RR_SPLIT (A/B runs) hands them to
+  // a separate rerank_kernel launch instead
+  static const bool rr_split = getenv("BB_RR_SPLIT") != nullptr;
+  if ((rr_c || rr_f) && rr_split &&
       ((rc = x->rr_out.ensure((size_t)Bc * kRrCap * 8)) || (rc = x->rr_cnt.ensure((size_t)Bc * 4)) ||
        (rc = x->rr_thr.ensure((size_t)Bc * 8)) || (rc = x->rr_r0.ensure((size_t)Bc * kRrR0Cap * 4)) ||
        (rc = x->rr_r0n.ensure((size_t)Bc * 4))))
@@ -709,7 +714,17 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
                                       ((uintptr_t)rows_c & 15) == 0));
     const bool fuse_f = !no_fuse && scan_f && x->dtype == F32 && q->q_cf_dtype == F32 && x->r % 4 == 0 && rows_f &&
                         ((uintptr_t)rows_f & 15) == 0;
-    if (need_content && !fuse_c) {
+    // exact re-rank on scan2 (query chunks <= 128 rows): the scan's prologue rounds the f32
+    // query rows (raw, or the liked sets' stored rows) to the bf16 operand itself and its
+    // chunk-0 workgroups write the f32 rows + ε the select needs — no prep launch
+    // (opt-in, BB_RR_FUSE_PREP: the per-lane query loads of the prologue cost more than the
+    // prep launch they replace — r02s: scan 20.8 -> 33.8 us vs prep 7.6 us at configs[1])
+    static const bool rr_fuse_prep = getenv("BB_RR_FUSE_PREP") != nullptr;
+    const bool rrfuse_c = rr_fuse_prep && !no_fuse && rr_c && !scan4_used(BF16, bpad) &&
+                          (gather_c || (q->q_dtype == F32 && x->d % 4 == 0 && rows_c && ((uintptr_t)rows_c & 15) == 0));
+    const bool rrfuse_f = rr_fuse_prep && !no_fuse && rr_f && !scan4_used(BF16, bpad) && q->q_cf_dtype == F32 && x->r % 4 == 0 &&
+                          rows_f && ((uintptr_t)rows_f & 15) == 0;
+    if (need_content && !fuse_c && !rrfuse_c) {
       PrepArgs pa{};
       pa.Bpad = bpad;
       pa.B = bc;
@@ -738,7 +753,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       }
       if ((rc = timed(x, K_PREP, s, [&] { return launch_prep(pa, s); }))) return rc;
     }
-    if (need_cf && !fuse_f) {
+    if (need_cf && !fuse_f && !rrfuse_f) {
       PrepArgs pa{};
       pa.Bpad = bpad;
       pa.B = bc;
@@ -824,6 +839,25 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
             ga.q_normalize = !cf_side && q->mode == BB_MODE_SEMANTIC;
           }
         }
+        if (cf_side ? rrfuse_f : rrfuse_c) {
+          ga.q_istats = (const float*)x->rr_stats.p + (cf_side ? 4 : 0);
+          ga.q_f32_out = (float*)(cf_side ? x->qcf32.p : x->qf32.p);
+          ga.q_f32_ld = cf_side ? x->Rpad : x->Dpad;
+          ga.q_eps_out = (float*)(cf_side ? x->qcfeps.p : x->qeps.p);
+          if (!cf_side && gather_c) {  // the stored f32 rows (normalised, zero padded)
+            ga.q_ids = (const int64_t*)d_items + b0;
+            ga.q_id_offset = x->id_offset;
+            ga.q_n_items = x->n;
+            ga.q_items_base = x->items.p;
+            ga.q_src_ld = x->Dpad;
+            ga.q_d = x->Dpad;
+          } else {
+            ga.q_src = cf_side ? rows_f : rows_c;
+            ga.q_d = cf_side ? x->r : x->d;
+            ga.q_src_ld = ga.q_d;
+            ga.q_normalize = !cf_side && q->mode == BB_MODE_SEMANTIC;
+          }
+        }
         DevBuf& planes = cf_side ? x->cf3 : x->items3;
         const bool rr_side = cf_side ? rr_f : rr_c;
         if (rr_side) {
@@ -901,11 +935,13 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           sa.rr_ld = cf_side ? x->Rpad : x->Dpad;
           sa.rr_d = (int)sa.rr_ld;
           sa.rr_gid_base = (uint32_t)x->id_offset;
-          sa.rr_out = (uint64_t*)x->rr_out.p;
-          sa.rr_cnt = (uint32_t*)x->rr_cnt.p;
-          sa.rr_thr = (uint32_t*)x->rr_thr.p;
-          sa.rr_r0 = (uint32_t*)x->rr_r0.p;
-          sa.rr_r0n = (uint32_t*)x->rr_r0n.p;
+          if (rr_split) {  // (A/B) hand-off buffers: a separate rerank_kernel launch finishes
+            sa.rr_out = (uint64_t*)x->rr_out.p;
+            sa.rr_cnt = (uint32_t*)x->rr_cnt.p;
+            sa.rr_thr = (uint32_t*)x->rr_thr.p;
+            sa.rr_r0 = (uint32_t*)x->rr_r0.p;
+            sa.rr_r0n = (uint32_t*)x->rr_r0n.p;
+          }
         }
         sa.carry_in = sl && !stream ? keys + ((size_t)(pp ^ 1) * sides + side) * side_keys : nullptr;
         sa.keys_out = pilot ? (uint64_t*)x->pilot.p : keys + ((size_t)pp * sides + side) * side_keys;
@@ -918,8 +954,69 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           sa.out_counts = o_cnt ? o_cnt + b0 : nullptr;
           sa.k_final = q->k;
         }
+        // BB_SELECT_TRACE (probe runs): per-phase s_memrealtime stamps of every query row,
+        // averaged over the rows and printed to stderr
+        static const bool sel_trace = getenv("BB_SELECT_TRACE") != nullptr;
+        if (sel_trace) {
+          if ((rc = x->trace.ensure((size_t)bc * 8 * 8))) return rc;
+          BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 64, s));
+          sa.trace = (uint64_t*)x->trace.p;
+        }
+        // one-slab re-rank of query chunks > 256 rows: one wave per query (select_rr_wave_kernel;
+        // the rows it leaves — caps overflowed — go to the block select, which skips the
+        // others).  Measured (r02y): B=1024 10.2 -> 10.5 M q/s, B=4096 10.9 -> 11.9 M q/s in
+        // flight; at B <= 256 the block select's four waves per query win on latency (19 vs
+        // 34 us per query).  BB_SELECT_WAVE=0/1 (A/B runs) forces it off / on.
+        static const int sel_wave_env = getenv("BB_SELECT_WAVE") ? atoi(getenv("BB_SELECT_WAVE")) : -1;
+        const bool sel_wave = rr_side && !rr_split && !sa.carry_in && ncols <= 32768 && K_int <= 256 &&
+                              (!sa.out_scores || q->k <= 256) &&
+                              (sel_wave_env == 1 || (sel_wave_env != 0 && bc > 256));
+        if (sel_wave) {
+          if ((rc = x->rr_flags.ensure((size_t)Bc * 4))) return rc;
+          sa.rr_flags = (uint32_t*)x->rr_flags.p;
+          if ((rc = timed(x, K_SELECT, s, [&] { return launch_select_rr_wave(sa, bc, s); }))) return rc;
+          if (sel_trace) {  // wave select phases: bound, tile list, gather, rescore, emit
+            std::vector<uint64_t> tr((size_t)bc * 8);
+            BB_HIP(hipMemcpyAsync(tr.data(), x->trace.p, tr.size() * 8, hipMemcpyDeviceToHost, s));
+            BB_HIP(hipStreamSynchronize(s));
+            double acc[8] = {0};
+            int rows = 0;
+            for (int i = 0; i < bc; ++i) {
+              const uint64_t* t = &tr[(size_t)i * 8];
+              if (!t[5]) continue;  // left to the block select
+              ++rows;
+              for (int j = 1; j < 6; ++j) acc[j] += (double)(t[j] - t[0]);
+              acc[6] += (double)t[6];
+              acc[7] += (double)t[7];
+            }
+            rows = std::max(rows, 1);
+            fprintf(stderr, "[bb wave select trace] rows=%d us-from-start: bound %.2f tiles %.2f gather %.2f "
+                    "rescore %.2f end %.2f  cands %.1f tiles %.1f\n", rows, acc[1] / rows / 100, acc[2] / rows / 100,
+                    acc[3] / rows / 100, acc[4] / rows / 100, acc[5] / rows / 100, acc[6] / rows, acc[7] / rows);
+            BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 64, s));
+          }
+        }
         if ((rc = timed(x, K_SELECT, s, [&] { return launch_select(sa, bc, s); }))) return rc;
-        if (rr_side && (rc = timed(x, K_RERANK, s, [&] { return launch_rerank(sa, bc, s); }))) return rc;
+        if (sel_trace) {
+          std::vector<uint64_t> tr((size_t)bc * 8);
+          BB_HIP(hipMemcpyAsync(tr.data(), x->trace.p, tr.size() * 8, hipMemcpyDeviceToHost, s));
+          BB_HIP(hipStreamSynchronize(s));
+          double acc[8] = {0};
+          uint64_t t0 = ~0ull, t1 = 0;
+          for (int i = 0; i < bc; ++i) {
+            const uint64_t* t = &tr[(size_t)i * 8];
+            for (int j = 1; j < 6; ++j) acc[j] += t[j] ? (double)(t[j] - t[0]) : 0.0;
+            acc[7] += t[7] ? (double)(t[7] - t[0]) : 0.0;
+            acc[6] += t[6] ? (double)(t[6] - t[0]) : 0.0;
+            t0 = std::min(t0, t[0]);
+            t1 = std::max(t1, t[7] ? t[7] : t[5]);
+          }
+          fprintf(stderr, "[bb select trace] rows=%d us-from-start: maxima %.2f bound %.2f tiles %.2f gather %.2f "
+                  "pre-finish %.2f rescored %.2f end %.2f  span %.2f us\n", bc, acc[1] / bc / 100, acc[2] / bc / 100,
+                  acc[3] / bc / 100, acc[4] / bc / 100, acc[5] / bc / 100, acc[6] / bc / 100, acc[7] / bc / 100,
+                  (double)(t1 - t0) / 100);
+        }
+        if (rr_side && rr_split && (rc = timed(x, K_RERANK, s, [&] { return launch_rerank(sa, bc, s); }))) return rc;
         final_pp = pp;
       }
     }

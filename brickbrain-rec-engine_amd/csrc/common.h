@@ -24,6 +24,14 @@ __host__ __device__ inline uint64_t make_key(uint32_t ord, uint32_t gid) {
 __host__ __device__ inline uint32_t gid_of(uint64_t key) { return 0xFFFFFFFFu - (uint32_t)key; }
 __host__ __device__ inline uint32_t ordk_of(uint64_t key) { return (uint32_t)(key >> 32); }
 
+// round-to-nearest-even f32 -> bf16 (NaN kept NaN)
+__device__ __forceinline__ uint16_t to_bf16(float f) {
+  uint32_t u = __builtin_bit_cast(uint32_t, f);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
 // ---- tiling constants ---------------------------------------------------------------------
 constexpr int kTileRows = 128;     // item / query rows are padded to this multiple
 constexpr int kSelectThreads = 256;
@@ -59,6 +67,14 @@ struct GemmArgs {
   int64_t q_src_ld;
   int32_t q_d;              // real query width (chunks past it read as 0)
   int32_t q_normalize;      // L2-normalise q_src rows
+  // fused re-rank operands (q_istats set; bf16 scan2 over the bf16 copy of an f32 index):
+  // the queries — raw f32 rows q_src, or with q_ids the f32 item rows at q_items_base, both
+  // with stride q_src_ld — are rounded to bf16 in-kernel; the workgroups of item chunk 0 also
+  // write the f32 rows and the bound ε of each query (as prep_kernel's out_f32 / eps_out)
+  const float* q_istats;    // item error statistics (rr_prepare_kernel), or null
+  float* q_f32_out;         // [Mpad][q_f32_ld]
+  int64_t q_f32_ld;
+  float* q_eps_out;         // [Mpad]
   uint64_t* trace;          // probe builds only (scan3 ABL & 256): per-workgroup timestamps
   // streaming top-K (scan ABL & kScanStream): no S slab; every eligible score whose order
   // image reaches the query's bound is appended to a private per-lane candidate region
@@ -143,12 +159,16 @@ struct SelectArgs {
   int64_t rr_ld;
   int32_t rr_d;             // elements of a row to dot (multiple of 4, <= rr_ld)
   uint32_t rr_gid_base;     // global id of local row 0 (the index's id_offset)
-  // hand-off from select_kernel to rerank_kernel
+  // hand-off from select_kernel to a separate rerank_kernel launch (BB_RR_SPLIT A/B runs);
+  // rr_out == null: select_kernel rescores and emits itself (the default)
   uint64_t* rr_out;         // [B][kRrCap] approximate candidate keys within 2ε of the K-th
   uint32_t* rr_cnt;         // [B] candidates, or kRrSlow (masses at the bound: exact slow path)
   uint32_t* rr_thr;         // [B][2] order images: gather bound (slow path), rank-0 bound
   uint32_t* rr_r0;          // [B][kRrR0Cap] rank-0 candidate global ids
   uint32_t* rr_r0n;         // [B] their count, or kRrSlow
+  // one-wave re-rank select (select_rr_wave_kernel): 1 = the row overflowed a cap and is left
+  // to the block select, which then skips every row whose flag is 0
+  uint32_t* rr_flags;       // [B] or null
 };
 constexpr int kRrCap = 512;
 constexpr int kRrR0Cap = 64;
@@ -241,6 +261,8 @@ int gemm_tile_n(int dtype);
 int gemm_tile_k(int dtype);
 hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s);
 hipError_t launch_rerank(const SelectArgs& a, int B, hipStream_t s);  // after launch_select, rr_* set
+// one wave per query, one-slab re-rank searches (rr_flags set; rows it leaves: launch_select)
+hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s);
 hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s);

@@ -130,6 +130,9 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   const int bm = gemm_tile_m(dtype), bn = gemm_tile_n(dtype), bk = gemm_tile_k(dtype);
   if (a.Mpad % bm || a.Ncols % bn || a.Kpad % bk || a.Mpad <= 0 || a.Ncols <= 0 || (a.slab_start & 31))
     return hipErrorInvalidValue;
+  // the fused re-rank prologue lives in scan2 (bf16, query chunks of <= 128 rows) only
+  if (a.q_istats && (dtype != BF16 || scan4_used(BF16, a.Mpad) || !a.q_f32_out || !a.q_eps_out || a.cand))
+    return hipErrorInvalidValue;
   if (gemm_uses_scan(dtype, a.Mpad, a.Kpad)) {
     if (dtype == BF16 ? launch_scan<uint16_t>(a, s) : launch_scan<float>(a, s)) return hipGetLastError();
   }

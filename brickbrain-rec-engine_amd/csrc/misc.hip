@@ -15,13 +15,6 @@ __device__ __forceinline__ double load_elem_d(const void* p, int dtype, size_t i
   if (dtype == F64) return ((const double*)p)[i];
   return (double)load_elem(p, dtype, i);
 }
-// round-to-nearest-even f32 -> bf16 (NaN kept NaN)
-__device__ __forceinline__ uint16_t to_bf16(float f) {
-  uint32_t u = __builtin_bit_cast(uint32_t, f);
-  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
 __device__ __forceinline__ void store_elem(void* p, int dtype, size_t i, float v) {
   if (dtype == BF16)
     ((uint16_t*)p)[i] = to_bf16(v);

@@ -30,14 +30,121 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(std::make_integer_sequence<int, N>{}, f);
 }
 
+// Exact re-rank prologue (bf16 operand from raw f32 rows, GemmArgs.q_f32_out): lane half h
+// of query row q holds elements (2u + h)·8 .. +8 of the row.  Normalised in f64 as prep_kernel
+// (sklearn normalize); rounded to bf16 (v_cvt_pk_bf16_f32, RNE).
+// With rr_write (the workgroups of item chunk 0) the f32 row and ε go out as well:
+// ε = E_x·|q̃| + N_x·|q̃−q| + γ·Ñ_x·|q̃| (prep_kernel's RrAcc), with the f32 sums of squares
+// scaled by (1 + 2^-10) to cover their rounding (<= 193 terms of 2^-24 each).
+// Source: raw rows q_src [M][q_src_ld], or (q_ids) the stored f32 item rows of the liked
+// sets, q_items_base [n][q_src_ld] (already normalised; an unknown id gives a zero row).
+template <int U>
+__device__ __forceinline__ void scan2_rr_prologue(const GemmArgs& a, int q, int h, bool rr_write, uint4 (&qf)[U]) {
+  typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+  bool ok = true;
+  const float* row;
+  if (a.q_ids) {
+    const int64_t lid = a.q_ids[q] - a.q_id_offset;
+    ok = lid >= 0 && lid < a.q_n_items;
+    row = (const float*)a.q_items_base + (size_t)(ok ? lid : 0) * a.q_src_ld;
+  } else {
+    row = (const float*)a.q_src + (size_t)q * a.q_src_ld;
+  }
+  const int d = a.q_d;
+  auto load = [&](int u, int s) -> float4 {  // (host: d % 4 == 0, 16-B aligned rows): clamp, load, select
+    const int k0 = (2 * u + h) * 8 + 4 * s;
+    const float4 t = *(const float4*)(row + (k0 < d ? k0 : d - 4));
+    return ok && k0 < d ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  // rows up to 384 wide stay in registers; wider ones are summed first and loaded again
+  constexpr bool kTwoPass = U > 24;
+  float4 x[kTwoPass ? 1 : 2 * U];
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const float4 v = load(u, s);
+      if (!kTwoPass) x[2 * u + s] = v;
+      if (a.q_normalize) {
+        s0 = fma((double)v.x, (double)v.x, s0);
+        s1 = fma((double)v.y, (double)v.y, s1);
+        s0 = fma((double)v.z, (double)v.z, s0);
+        s1 = fma((double)v.w, (double)v.w, s1);
+      }
+    }
+  // f64 norm, f64 reciprocal: the f32 element is (float)(x·(1/‖x‖)), prep_kernel's
+  // (float)(x/‖x‖) but at the ~2^-28 of elements whose quotient falls on an f32 rounding
+  // boundary to within the f64 error
+  double inv = 1.0;
+  bool scale = false;
+  if (a.q_normalize) {
+    double ss = s0 + s1;
+    ss += __shfl_xor(ss, 32);
+    const double nrm = sqrt(ss);
+    scale = nrm != 0.0;
+    inv = scale ? 1.0 / nrm : 1.0;
+  }
+  auto scl = [&](float v) -> float { return scale ? (float)((double)v * inv) : v; };
+  // per k-step: scale, round to the bf16 operand; chunk 0 also stores the f32 row and sums
+  // the squares of the rounding error and of the operand
+  float* orow = a.q_f32_out + (size_t)q * a.q_f32_ld;
+  float e2 = 0.f, b2 = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float4 p = kTwoPass ? load(u, 0) : x[2 * u], r = kTwoPass ? load(u, 1) : x[2 * u + 1];
+    p = make_float4(scl(p.x), scl(p.y), scl(p.z), scl(p.w));
+    r = make_float4(scl(r.x), scl(r.y), scl(r.z), scl(r.w));
+    const bf2v b0 = {(__bf16)p.x, (__bf16)p.y}, b1 = {(__bf16)p.z, (__bf16)p.w};
+    const bf2v b2v = {(__bf16)r.x, (__bf16)r.y}, b3 = {(__bf16)r.z, (__bf16)r.w};
+    qf[u] = make_uint4(__builtin_bit_cast(uint32_t, b0), __builtin_bit_cast(uint32_t, b1),
+                       __builtin_bit_cast(uint32_t, b2v), __builtin_bit_cast(uint32_t, b3));
+    if (rr_write) {
+      const uint32_t w[4] = {qf[u].x, qf[u].y, qf[u].z, qf[u].w};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int k0 = (2 * u + h) * 8 + 4 * s;
+        const float4 v = s ? r : p;
+        if (k0 < a.q_f32_ld) *(float4*)(orow + k0) = v;
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t ww = w[2 * s + (c >> 1)];
+          const float bv = __uint_as_float((c & 1) ? (ww & 0xFFFF0000u) : (ww << 16));
+          const float e = vv[c] - bv;  // exact (bv is vv[c] rounded to 8 significant bits)
+          e2 = fmaf(e, e, e2);
+          b2 = fmaf(bv, bv, b2);
+        }
+      }
+    }
+  }
+  if (!rr_write) return;
+  e2 += __shfl_xor(e2, 32);
+  b2 += __shfl_xor(b2, 32);
+  if (h == 0) {
+    const double sc = 1.0 + 0x1p-10;
+    const double e = sqrt((double)e2 * sc), b = sqrt((double)b2 * sc);
+    const double gam = 2.0 * (double)a.Kpad * 0x1p-24;
+    const double eps = (double)a.q_istats[0] * b + (double)a.q_istats[1] * e + gam * (double)a.q_istats[2] * b;
+    a.q_eps_out[q] = __double2float_ru(eps * (1.0 + 0x1p-20));
+  }
+}
+
 // Query operand: 16-B chunk (2u + h) of this lane's query row into qf[u].
 template <typename T, int KU>
-__device__ __forceinline__ void scan2_load_queries(const GemmArgs& a, int q, int h, uint4 (&qf)[KU / 2]) {
+__device__ __forceinline__ void scan2_load_queries(const GemmArgs& a, int q, int h, uint4 (&qf)[KU / 2],
+                                                   bool rr_write = false) {
   constexpr int U = KU / 2;
   if (q >= a.M_valid) {
 #pragma unroll
     for (int u = 0; u < U; ++u) qf[u] = make_uint4(0, 0, 0, 0);
     return;
+  }
+  if constexpr (sizeof(T) == 2 && KU <= kRrMaxD / 8) {
+    if (a.q_istats) {  // exact re-rank operands (GemmArgs.q_f32_out)
+      scan2_rr_prologue<U>(a, q, h, rr_write, qf);
+      return;
+    }
   }
   if (a.q_ids) {  // similar / hybrid: the stored (normalised, padded) item row of the liked set
     const int64_t lid = a.q_ids[q] - a.q_id_offset;
@@ -230,7 +337,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   if (tile_lo >= tile_hi) return;  // uniform per workgroup
 
   uint4 qf[U];
-  scan2_load_queries<T, KU>(a, q, h, qf);
+  scan2_load_queries<T, KU>(a, q, h, qf, chunk == 0 && a.q_istats != nullptr);
   float qa[sizeof(T) == 4 ? 4 * U : 1];  // f32: the operand as 4U scalars, pinned to AGPRs
   if constexpr (sizeof(T) == 4) {
 #pragma unroll

@@ -34,7 +34,8 @@ constexpr int kOffTlist = kOffTmax + kSelectThreads * 4;
 constexpr int kOffMisc = kOffTlist + kTileCap * 4;
 constexpr int kOffR0 = kOffMisc + 256;          // re-rank: rank-0 tile list
 constexpr int kR0Cap = 32;
-constexpr int kSelectLds = kOffR0 + kR0Cap * 4;
+constexpr int kOffQs = kOffR0 + kR0Cap * 4;       // fused re-rank: the f32 query row
+constexpr int kSelectLds = kOffQs + kRrMaxD * 4;
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -247,7 +248,7 @@ __device__ __forceinline__ void wave_bitonic_desc(uint64_t (&v)[E], int lane) {
 
 // Sort cnt (<= 64·E) candidates with one wave and emit the final list / the key list.
 template <int E>
-__device__ void wave_sort_emit(const uint64_t* cand, int cnt, const SelectArgs& a, int row, uint64_t gmax) {
+__device__ __forceinline__ void wave_sort_emit(const uint64_t* cand, int cnt, const SelectArgs& a, int row, uint64_t gmax) {
   const int lane = threadIdx.x & 63;
   uint64_t v[E];
 #pragma unroll
@@ -297,62 +298,45 @@ __device__ __forceinline__ uint32_t ord_sub(uint32_t o, float m) {
   const uint32_t r = ord_of(g);
   return r > 1u ? r : 1u;
 }
-// Exact score of one item row against the query row: f32 products summed in f64 as 16
-// lane partials (partial p takes float4 chunks p, p+16, ... in order) combined by the xor
-// tree of 8, 4, 2, 1 — one fixed order, so every path (grouped or per-thread) gives the
-// same bits.  Loads are issued unconditionally (clamped index, masked contribution) so all
-// of a row's chunks are in flight together.
+// Exact score of one item row against the query row: f32 products summed in f64, 16 lanes
+// per row — lane p takes the float4 chunks p, p+16, ... in order, the 16 partials are then
+// combined by DPP (quad swaps, row half-mirror, row mirror) — one fixed order for every path
+// (candidates, rank 0, slow paths), so an item rescored twice gets the same bits.
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4v lds_f4(const float* qs, int c) {
   return *(const __attribute__((address_space(3))) f4v*)((const __attribute__((address_space(3))) char*)
                                                             ((size_t)(const void*)qs) + c * 16);
 }
-__device__ __forceinline__ double fma4(const f4v& x, const f4v& q, double acc) {
-  acc = fma((double)x.x, (double)q.x, acc);
-  acc = fma((double)x.y, (double)q.y, acc);
-  acc = fma((double)x.z, (double)q.z, acc);
-  return fma((double)x.w, (double)q.w, acc);
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ float rr_dot_thread(const float* xrow, const float* qs, int nch) {
-  const f4v* xr = (const f4v*)xrow;
-  double s[16];
-#pragma unroll
-  for (int p = 0; p < 16; ++p) s[p] = 0.0;
-  for (int base = 0; base < nch; base += 16) {
-#pragma unroll
-    for (int h = 0; h < 16; h += 8) {   // 8 chunks in flight: partials h..h+7
-      f4v xv[8];
-#pragma unroll
-      for (int p = 0; p < 8; ++p) xv[p] = xr[min(base + h + p, nch - 1)];
-#pragma unroll
-      for (int p = 0; p < 8; ++p)
-        if (base + h + p < nch) s[h + p] = fma4(xv[p], lds_f4(qs, base + h + p), s[h + p]);
-    }
-  }
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1)
-#pragma unroll
-    for (int p = 0; p < o; ++p) s[p] = s[p] + s[p + o];
-  return (float)s[0];
+__device__ __forceinline__ double sum16_f64(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror: quad 0 <-> 1, 2 <-> 3
+  v += dpp_f64<0x140>(v);  // row_mirror: half 0 <-> 1
+  return v;
 }
 __device__ __forceinline__ uint64_t rr_key(float e, uint32_t gid) { return make_key(ord_of(e + 0.0f), gid); }
 
-// Rescore keys[0..m) in place (approximate -> exact keys): 16 lanes per candidate, each
-// group with U candidates' rows in flight at once; the query chunks of the lane stay in
-// registers.
-template <int CPL>
-__device__ void rr_rescore(uint64_t* keys, int m, const SelectArgs& a, const float* qs) {
-  constexpr int U = CPL <= 6 ? 4 : CPL <= 8 ? 2 : 1;  // <= 24 row chunks in flight per lane
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int p = lane & 15, g = wave * 4 + (lane >> 4);   // 16 groups per workgroup
+// Rescore keys[0..m) in place (approximate / placeholder -> exact keys).  NG lane groups of
+// 16 (NG·16 threads call it together), U rows per group in flight; the lane's query chunks
+// are held in f64.
+template <int CPL, int U, int NG>
+__device__ __forceinline__ void rescore_rows(uint64_t* keys, int m, const SelectArgs& a, const float* qs, int t) {
+  const int p = t & 15, g = t >> 4;
   const int nch = a.rr_d >> 2;
-  f4v qv[CPL];
+  double qd[CPL][4];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
     const int c = p + 16 * j;
-    qv[j] = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
+    const f4v v = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
+    qd[j][0] = v.x, qd[j][1] = v.y, qd[j][2] = v.z, qd[j][3] = v.w;
   }
-  for (int c0 = g * U; c0 < m; c0 += 16 * U) {
+  for (int c0 = g * U; c0 < m; c0 += NG * U) {
     uint32_t gid[U];
     f4v xv[U][CPL];
 #pragma unroll
@@ -367,35 +351,44 @@ __device__ void rr_rescore(uint64_t* keys, int m, const SelectArgs& a, const flo
       double acc = 0.0;
 #pragma unroll
       for (int j = 0; j < CPL; ++j)
-        if (p + 16 * j < nch) acc = fma4(xv[u][j], qv[j], acc);
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (p + 16 * j < nch) {
+          acc = fma((double)xv[u][j].x, qd[j][0], acc);
+          acc = fma((double)xv[u][j].y, qd[j][1], acc);
+          acc = fma((double)xv[u][j].z, qd[j][2], acc);
+          acc = fma((double)xv[u][j].w, qd[j][3], acc);
+        }
+      acc = sum16_f64(acc);
       if (p == 0 && c0 + u < m) keys[c0 + u] = rr_key((float)acc, gid[u]);
     }
   }
 }
+// block select (256 threads): one round for up to 96 rows at d <= 384
 __device__ __forceinline__ void rr_rescore_any(uint64_t* keys, int m, const SelectArgs& a, const float* qs) {
   const int cpl = ((a.rr_d >> 2) + 15) >> 4;
-  if (cpl <= 2) rr_rescore<2>(keys, m, a, qs);
-  else if (cpl <= 4) rr_rescore<4>(keys, m, a, qs);
-  else if (cpl <= 6) rr_rescore<6>(keys, m, a, qs);
-  else rr_rescore<8>(keys, m, a, qs);   // rows up to kRrMaxD = 512 wide
+  const int t = threadIdx.x;
+  if (cpl <= 1) rescore_rows<1, 8, 16>(keys, m, a, qs, t);
+  else if (cpl <= 2) rescore_rows<2, 8, 16>(keys, m, a, qs, t);
+  else if (cpl <= 4) rescore_rows<4, 6, 16>(keys, m, a, qs, t);
+  else if (cpl <= 6) rescore_rows<6, 6, 16>(keys, m, a, qs, t);
+  else rescore_rows<8, 4, 16>(keys, m, a, qs, t);   // rows up to kRrMaxD = 512 wide
 }
 
 // Re-rank with masses of items at the gather bound (more than kCandCap): an exact running
-// top-K over every eligible item whose approximate score reaches Tg, rescored one item per
-// thread and merged into the list 1024+ keys at a time; then the final list / key list.
+// top-K over every eligible item whose approximate score reaches Tg, collected 256 per round,
+// rescored in batches (rr_rescore_any, 16 lanes per row) and merged into the list 1024+ keys
+// at a time; then the final list / key list.
 template <typename Elig, typename SAt>
-__device__ void rr_slow_path(const SelectArgs& a, int row, int n, uint32_t Tg, int K, uint64_t* cand, uint32_t* misc,
-                             const float* qs, Elig elig, SAt s_at) {
+__device__ __forceinline__ void rr_slow_path(const SelectArgs& a, int row, int n, uint32_t Tg, int K, uint64_t* cand,
+                                             uint32_t* misc, const float* qs, Elig elig, SAt s_at) {
   const int tid = threadIdx.x;
   uint64_t* sel = cand + 2048;  // the running list: K <= kMaxKInt keys, sorted desc
   uint64_t* buf = cand;         // fresh keys [0, nb) + the list appended for the merge
   for (int i = tid; i < K; i += kSelectThreads) sel[i] = 0ull;
   if (tid == 0) misc[12] = 0;
   __syncthreads();
-  auto merge = [&]() {
-    const int nb = (int)misc[12];
+  auto merge = [&](int nb) {
+    rr_rescore_any(buf, nb, a, qs);  // placeholder keys -> exact keys
+    __syncthreads();
     for (int i = tid; i < K; i += kSelectThreads) buf[nb + i] = sel[i];
     int P = 1;
     while (P < nb + K) P <<= 1;
@@ -409,15 +402,17 @@ __device__ void rr_slow_path(const SelectArgs& a, int row, int n, uint32_t Tg, i
   };
   for (int base = 0; base < n; base += kSelectThreads) {
     const int j = base + tid;
-    if (j < n && ((elig(j >> 5) >> (j & 31)) & 1u) && ord_of(s_at(j)) >= Tg) {
-      const uint32_t gid = a.gid0 + (uint32_t)j;
-      const uint64_t k = rr_key(rr_dot_thread(a.rr_x + (size_t)(gid - a.rr_gid_base) * a.rr_ld, qs, a.rr_d >> 2), gid);
-      buf[atomicAdd(&misc[12], 1u)] = k;
-    }
+    if (j < n && ((elig(j >> 5) >> (j & 31)) & 1u) && ord_of(s_at(j)) >= Tg)
+      buf[atomicAdd(&misc[12], 1u)] = make_key(1u, a.gid0 + (uint32_t)j);
     __syncthreads();
-    if (misc[12] > 2048u - kMaxKInt - kSelectThreads) merge();
+    const int nb = (int)misc[12];
+    __syncthreads();  // every thread holds nb before the next round's appends
+    if (nb > 2048 - kMaxKInt - kSelectThreads) merge(nb);
   }
-  if (misc[12]) merge();
+  {
+    const int nb = (int)misc[12];
+    if (nb) merge(nb);
+  }
   const uint64_t gmax = *(const uint64_t*)(misc + 10);
   int cnt = 0;
   for (int i = 0; i < K; ++i) cnt += sel[i] != 0ull;  // uniform: every thread counts
@@ -440,7 +435,9 @@ __device__ void rr_slow_path(const SelectArgs& a, int row, int n, uint32_t Tg, i
 __device__ const uint32_t kWordOnes = 0xFFFFFFFFu;
 __device__ const uint32_t kWordZero = 0u;
 
-template <int ABL>
+// RR: the re-rank variant (rr_eps set) — a separate instance, so the plain select keeps its
+// register budget
+template <int ABL, bool RR = false>
 __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   __shared__ __attribute__((aligned(16))) char dsm[kSelectLds];
   uint64_t* cand = (uint64_t*)dsm;
@@ -452,6 +449,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   uint64_t* red = (uint64_t*)(misc + 32);         // 4 u64
 
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (RR && a.rr_flags && a.rr_flags[row] == 0u) return;  // finished by select_rr_wave_kernel
   const int n = a.n_cols, K = a.K;
   const int ntiles = (n + 31) >> 5;
   const float* Srow = a.S + (size_t)row * a.lds;
@@ -482,7 +480,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     if (a.trace && tid == 0) a.trace[row * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  const bool rr = a.rr_eps != nullptr;
+  constexpr bool rr = RR;
   float eps2 = 0.f;
   if (rr) eps2 = rr_margin(a.rr_eps[row]);
   if (tid == 0) {
@@ -501,6 +499,12 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     v0[b] = t < ntiles ? trow[t] : 0u;
     p0[b] = (prow && t < ntiles) ? prow[t] : 0u;
   }
+  // fused re-rank: the f32 query row goes to LDS (issued behind the maxima loads, so its
+  // wait is theirs)
+  float* qs = (float*)(dsm + kOffQs);
+  const bool rr_fused = RR && a.rr_out == nullptr;
+  float4 qv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (rr_fused && tid < (a.rr_d >> 2)) qv = ((const float4*)(a.rr_q + (size_t)row * a.rr_ld))[tid];
   uint32_t tm = 0;
   uint64_t best = 0;  // (present max << 32) | ~tile : larger = higher ord, then lower tile
 #pragma unroll
@@ -520,6 +524,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
     }
   }
   tmx[tid] = tm;
+  if (rr_fused && tid < (a.rr_d >> 2)) ((float4*)qs)[tid] = qv;
   if (prow) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -700,16 +705,19 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   stamp(4);
   uint32_t cnt = misc[7];
   if constexpr (ABL == 4) { if (cnt == 0x12345u) a.keys_out[row] = cnt; return; }
-  if (rr) {
-    // ---- re-rank hand-off (rerank_kernel rescores and emits).  Rank 0: the present items
-    // whose approximate score is within the margin of the approximate present maximum
-    // (typically the liked set alone) ----
+  if constexpr (rr) {
+    // ---- exact re-rank.  Fused (rr_out == null): this workgroup rescores the candidates
+    // from the f32 rows and emits (rr_finish); otherwise the hand-off to rerank_kernel.
+    // Rank 0: the present items whose approximate score is within the margin of the
+    // approximate present maximum (typically the liked set alone) ----
+    const bool fuse = a.rr_out == nullptr;
+    uint32_t r0n = 0, thr0 = 0;
     if (prow) {
       uint64_t b = red[0];
 #pragma unroll
       for (int i = 1; i < kSelectThreads / 64; ++i) b = red[i] > b ? red[i] : b;
       const uint32_t Pm = (uint32_t)(b >> 32);
-      const uint32_t thr0 = ord_sub(Pm, eps2);
+      thr0 = ord_sub(Pm, eps2);
       uint32_t* r0t = (uint32_t*)(dsm + kOffR0);
       if (Pm) {
 #pragma unroll
@@ -729,69 +737,110 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
       if (tid == 0) misc[14] = 0;
       __syncthreads();
       const uint32_t nt0 = misc[13];
-      uint32_t* r0g = a.rr_r0 + (size_t)row * kRrR0Cap;
+      uint32_t* r0g = fuse ? nullptr : a.rr_r0 + (size_t)row * kRrR0Cap;
       if (Pm && nt0 <= (uint32_t)kR0Cap)
         for (int i = tid; i < (int)nt0 * 32; i += kSelectThreads) {
           const int t = (int)r0t[i >> 5], it = i & 31, j = t * 32 + it;
           const uint32_t pw = a.present ? a.present[w0 + t] : ~0u;
           if (j < n && ((pw >> it) & 1u) && ord_of(s_at(j)) >= thr0) {
             const uint32_t q = atomicAdd(&misc[14], 1u);
-            if (q < (uint32_t)kRrR0Cap) r0g[q] = a.gid0 + (uint32_t)j;
+            if (q < (uint32_t)kRrR0Cap) {
+              if (fuse) cand[2048 + q] = make_key(1u, a.gid0 + (uint32_t)j);
+              else r0g[q] = a.gid0 + (uint32_t)j;
+            }
           }
         }
       __syncthreads();
-      if (tid == 0) {
-        a.rr_r0n[row] = !Pm ? 0u : (nt0 > (uint32_t)kR0Cap || misc[14] > (uint32_t)kRrR0Cap) ? kRrSlow : misc[14];
+      r0n = !Pm ? 0u : (nt0 > (uint32_t)kR0Cap || misc[14] > (uint32_t)kRrR0Cap) ? kRrSlow : misc[14];
+      if (!fuse && tid == 0) {
+        a.rr_r0n[row] = r0n;
         a.rr_thr[2 * row + 1] = thr0;
       }
     }
-    if (cnt > (uint32_t)kCandCap) {  // masses of items at the bound: the exact slow path
-      if (tid == 0) {
-        a.rr_cnt[row] = kRrSlow;
-        a.rr_thr[2 * row] = Tg;
-      }
-      return;
-    }
-    // ---- approximate order -> the K-th approximate score -> the candidates within 2ε ----
-    if (cnt <= 256) {
+    uint32_t m = kRrSlow;  // masses of items at the bound: the exact slow path
+    if (cnt <= 256u) {
+      // ---- the K-th approximate score by ballots (wave 0, four candidates per lane), then
+      // the candidates within 2ε of it compacted to cand[0..m) — no sort needed here:
+      // rr_finish rescores and sorts them ----
       if (wave == 0) {
         uint64_t v[4];
+        uint32_t o[4];
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) v[s4] = s4 * 64 + lane < (int)cnt ? cand[s4 * 64 + lane] : 0ull;
-        wave_bitonic_desc<4>(v, lane);
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int i = s4 * 64 + lane;
+          v[s4] = i < (int)cnt ? cand[i] : 0ull;
+          o[s4] = ordk_of(v[s4]);
+        }
+        uint32_t thr = 1u;
+        if (cnt >= (uint32_t)K) {
+          auto cnt_ge = [&](uint32_t c) -> uint32_t {
+            return (uint32_t)(__popcll(__ballot(o[0] >= c)) + __popcll(__ballot(o[1] >= c)) +
+                              __popcll(__ballot(o[2] >= c)) + __popcll(__ballot(o[3] >= c)));
+          };
+          uint32_t hi = max(max(o[0], o[1]), max(o[2], o[3]));
+          uint32_t lo = min(min(o[0] ? o[0] : ~0u, o[1] ? o[1] : ~0u), min(o[2] ? o[2] : ~0u, o[3] ? o[3] : ~0u));
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-          if (s4 * 64 + lane < (int)cnt) cand[s4 * 64 + lane] = v[s4];
+          for (int sh = 32; sh > 0; sh >>= 1) {
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, sh));
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, sh));
+          }
+          hi = __builtin_amdgcn_readfirstlane(hi);
+          lo = __builtin_amdgcn_readfirstlane(lo);
+          const uint32_t dd = hi ^ lo;
+          const int top = dd ? 31 - __builtin_clz(dd) : -1;
+          uint32_t P = top < 0 ? hi : top >= 31 ? 0u : hi & ~((2u << top) - 1u);
+          for (int bt = top; bt >= 0; --bt) {
+            const uint32_t c = P | (1u << bt);
+            if (cnt_ge(c) >= (uint32_t)K) P = c;
+          }
+          thr = ord_sub(P, eps2);
+        }
+        uint32_t base = 0;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const bool keep = v[s4] != 0ull && o[s4] >= thr;
+          const uint64_t bm = __ballot(keep);
+          const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+          if (keep) cand[pos] = v[s4];
+          base += (uint32_t)__popcll(bm);
+        }
+        if (lane == 0) misc[12] = base;
       }
       __syncthreads();
-    } else {
+      m = misc[12];
+    } else if (cnt <= (uint32_t)kCandCap) {
+      // ---- approximate order -> the K-th approximate score -> the candidates within 2ε ----
       int P = 1;
       while (P < (int)cnt) P <<= 1;
       for (int i = (int)cnt + tid; i < P; i += kSelectThreads) cand[i] = 0ull;
       __syncthreads();
       bitonic_desc_u64(cand, P);
-    }
-    uint32_t m = cnt;
-    if (cnt >= (uint32_t)K) {
-      const uint32_t thr = ord_sub(ordk_of(cand[K - 1]), eps2);
-      // sorted: the prefix of keys reaching thr (thread-parallel boundary search)
-      if (tid == 0) misc[12] = cnt;
-      __syncthreads();
-      for (int i = tid; i < (int)cnt; i += kSelectThreads)
-        if (ordk_of(cand[i]) >= thr && (i + 1 == (int)cnt || ordk_of(cand[i + 1]) < thr)) misc[12] = (uint32_t)(i + 1);
-      __syncthreads();
-      m = misc[12];
-    }
-    if (m > (uint32_t)kRrCap) {
-      if (tid == 0) {
-        a.rr_cnt[row] = kRrSlow;
-        a.rr_thr[2 * row] = Tg;
+      m = cnt;
+      if (cnt >= (uint32_t)K) {
+        const uint32_t thr = ord_sub(ordk_of(cand[K - 1]), eps2);
+        // sorted: the prefix of keys reaching thr (thread-parallel boundary search)
+        if (tid == 0) misc[12] = cnt;
+        __syncthreads();
+        for (int i = tid; i < (int)cnt; i += kSelectThreads)
+          if (ordk_of(cand[i]) >= thr && (i + 1 == (int)cnt || ordk_of(cand[i + 1]) < thr)) misc[12] = (uint32_t)(i + 1);
+        __syncthreads();
+        m = misc[12];
       }
+    }
+    if (m > (uint32_t)kRrCap) m = kRrSlow;
+    if (fuse) {
+      stamp(5);
+      rr_finish(a, row, n, cand, misc, qs, m, r0n, Tg, thr0, elig, s_at);
+      stamp(7);
       return;
     }
+    if (tid == 0) {
+      a.rr_cnt[row] = m;
+      if (m == kRrSlow) a.rr_thr[2 * row] = Tg;
+    }
+    if (m == kRrSlow) return;
     uint64_t* out = a.rr_out + (size_t)row * kRrCap;
     for (int i = tid; i < (int)m; i += kSelectThreads) out[i] = cand[i];
-    if (tid == 0) a.rr_cnt[row] = m;
     return;
   } else if (cnt > (uint32_t)kCandCap) {
     __syncthreads();
@@ -1051,14 +1100,84 @@ constexpr int kRrOffQ = 2560 * 8;
 constexpr int kRrOffMisc = kRrOffQ + kRrMaxD * 4;
 constexpr int kRrLds = kRrOffMisc + 256;
 
+// Exact finish of a re-rank row (shared by select_kernel's fused path and rerank_kernel):
+// cand[0..m) holds the approximate candidates within 2ε of the K-th (m = kRrSlow: masses at
+// the gather bound Tg, the exact slow path), cand[2048..2048+n0) the rank-0 candidates
+// (n0 = kRrSlow: every present item within thr0 of the present maximum).  Rescores them from
+// the f32 rows, resolves rank 0 into max_inout and emits the final list / key list.
+template <typename Elig, typename SAt>
+__device__ __forceinline__ void rr_finish(const SelectArgs& a, int row, int n, uint64_t* cand, uint32_t* misc, const float* qs,
+                          uint32_t m, uint32_t n0, uint32_t Tg, uint32_t thr0, Elig elig, SAt s_at) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int K = a.K, ntiles = (n + 31) >> 5;
+  const int64_t w0 = a.slab_start >> 5;
+  if (tid == 0) *(uint64_t*)(misc + 10) = 0ull;
+  __syncthreads();
+  // ---- exact rank 0 ----
+  if (a.max_inout) {
+    uint64_t best0 = 0;
+    if (n0 != kRrSlow) {
+      rr_rescore_any(cand + 2048, (int)n0, a, qs);
+      __syncthreads();
+      for (int i = tid; i < (int)n0; i += kSelectThreads) best0 = cand[2048 + i] > best0 ? cand[2048 + i] : best0;
+    } else {  // masses of near-duplicates at the top: every present item within the margin,
+              // collected 256 per round into cand[2048..2560) and rescored in batches
+      const uint32_t* prow = a.pmax + (size_t)row * a.ldt;
+      uint64_t* rb = cand + 2048;
+      if (tid == 0) misc[15] = 0;
+      __syncthreads();
+      const int nall = ntiles * 32;
+      for (int base = 0; base < nall; base += kSelectThreads) {
+        const int i = base + tid;
+        if (i < n && prow[i >> 5] >= thr0) {
+          const int t = i >> 5, it = i & 31;
+          const uint32_t pw = a.present ? a.present[w0 + t] : ~0u;
+          if (((pw >> it) & 1u) && ord_of(s_at(i)) >= thr0) rb[atomicAdd(&misc[15], 1u)] = make_key(1u, a.gid0 + (uint32_t)i);
+        }
+        __syncthreads();
+        const int nb = (int)misc[15];
+        __syncthreads();  // every thread holds nb before the next round's appends
+        if (nb > 256 || (base + kSelectThreads >= nall && nb > 0)) {
+          rr_rescore_any(rb, nb, a, qs);
+          __syncthreads();
+          for (int k = tid; k < nb; k += kSelectThreads) best0 = rb[k] > best0 ? rb[k] : best0;
+          __syncthreads();
+          if (tid == 0) misc[15] = 0;
+          __syncthreads();
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t y = __shfl_xor(best0, o);
+      best0 = y > best0 ? y : best0;
+    }
+    if (lane == 0) atomicMax((unsigned long long*)(misc + 10), (unsigned long long)best0);
+    __syncthreads();
+    if (tid == 0) a.max_inout[row] = *(const uint64_t*)(misc + 10);
+  }
+  if (m == kRrSlow) {
+    rr_slow_path(a, row, n, Tg, K, cand, misc, qs, elig, s_at);
+    return;
+  }
+  rr_rescore_any(cand, (int)m, a, qs);
+  __syncthreads();
+  if (a.trace && threadIdx.x == 0) a.trace[row * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+  const uint64_t gmax = *(const uint64_t*)(misc + 10);
+  if (wave != 0) return;
+  if (m <= 64) wave_sort_emit<1>(cand, (int)m, a, row, gmax);
+  else if (m <= 128) wave_sort_emit<2>(cand, (int)m, a, row, gmax);
+  else if (m <= 256) wave_sort_emit<4>(cand, (int)m, a, row, gmax);
+  else wave_sort_emit<8>(cand, (int)m, a, row, gmax);
+}
+
 __global__ __launch_bounds__(kSelectThreads) void rerank_kernel(SelectArgs a) {
   __shared__ __attribute__((aligned(16))) char dsm[kRrLds];
   uint64_t* cand = (uint64_t*)dsm;
   float* qs = (float*)(dsm + kRrOffQ);
   uint32_t* misc = (uint32_t*)(dsm + kRrOffMisc);
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n = a.n_cols, K = a.K;
-  const int ntiles = (n + 31) >> 5;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int n = a.n_cols;
   const float* Srow = a.S + (size_t)row * a.lds;
   auto s_at = [&](int j) -> float {
     return a.s_blocked ? a.S[sblk_quad(row, j >> 5, (j >> 2) & 7, a.ldt) + (j & 3)] : Srow[j];
@@ -1083,50 +1202,253 @@ __global__ __launch_bounds__(kSelectThreads) void rerank_kernel(SelectArgs a) {
     if (n0 != kRrSlow)
       for (int i = tid; i < (int)n0; i += kSelectThreads) cand[2048 + i] = make_key(1u, a.rr_r0[(size_t)row * kRrR0Cap + i]);
   }
-  if (tid == 0) *(uint64_t*)(misc + 10) = 0ull;
   __syncthreads();
-  // ---- exact rank 0 ----
-  if (a.max_inout) {
-    uint64_t best0 = 0;
-    if (n0 != kRrSlow) {
-      rr_rescore_any(cand + 2048, (int)n0, a, qs);
-      __syncthreads();
-      for (int i = tid; i < (int)n0; i += kSelectThreads) best0 = cand[2048 + i] > best0 ? cand[2048 + i] : best0;
-    } else {  // masses of near-duplicates at the top: every present item within the margin
-      const uint32_t thr0 = a.rr_thr[2 * row + 1];
-      const uint32_t* prow = a.pmax + (size_t)row * a.ldt;
-      for (int i = tid; i < ntiles * 32; i += kSelectThreads) {
-        const int t = i >> 5, it = i & 31;
-        if (prow[t] < thr0) continue;
-        const uint32_t pw = a.present ? a.present[w0 + t] : ~0u;
-        if (i < n && ((pw >> it) & 1u) && ord_of(s_at(i)) >= thr0) {
-          const uint32_t gid = a.gid0 + (uint32_t)i;
-          const uint64_t k = rr_key(rr_dot_thread(a.rr_x + (size_t)(gid - a.rr_gid_base) * a.rr_ld, qs, a.rr_d >> 2), gid);
-          best0 = k > best0 ? k : best0;
-        }
-      }
+  rr_finish(a, row, n, cand, misc, qs, m, n0, a.rr_thr[2 * row], a.max_inout ? a.rr_thr[2 * row + 1] : 0u, elig, s_at);
+}
+
+// ---- one wave per query: the exact re-rank select of a one-slab search ----------------------
+// The block select above keeps four waves resident per query for ~25 us, mostly waiting on
+// memory; with three batches in flight that residency, not the scan, capped throughput
+// (r02t: 256 scan CUs x 18 us + 256 select workgroups x 25 us per batch).  Here one wave
+// carries a query through the whole chain and ~8 queries share a CU:
+//   maxima   lane l holds the eligible / present maxima of tiles l, l+64, ... (<= 16 each)
+//   bound    T0 = the K-th largest TILE maximum (ballot bit loop over 16 values per lane):
+//            tighter than the block select's per-thread bound, so ~K tiles qualify
+//   gather   tiles with maxima >= Tg = T0 - 2ε; their eligible items >= Tg (approximate keys)
+//   rank 0   (similar / hybrid content side) present items within 2ε of the present maximum
+//   rescore  every candidate and rank-0 item from the f32 rows (16 lanes per row, U rows in
+//            flight per lane group, f64 sums in rr_rescore's fixed order)
+//   emit     register bitonic sort, rank-0 drop, final list or key list
+// A query that overflows a cap (masses of near-ties) sets rr_flags[row]; the block select
+// then runs that row alone (its launch returns at once for every other row).
+constexpr int kWvTPL = 16;     // tile maxima per lane: slabs of up to 1024 tiles (32,768 columns)
+constexpr int kWvCand = 256;   // candidates (sorted by one wave in registers)
+constexpr int kWvTiles = 256;  // qualifying tiles
+constexpr int kWvR0 = 64;      // rank-0 items
+constexpr int kWvR0Tiles = 16;
+constexpr int kWvOffCand = 0;                              // u64 [kWvCand + kWvR0]
+constexpr int kWvOffTl = kWvOffCand + (kWvCand + kWvR0) * 8;  // u32 [kWvTiles]
+constexpr int kWvOffR0t = kWvOffTl + kWvTiles * 4;        // u32 [kWvR0Tiles]
+constexpr int kWvOffQs = kWvOffR0t + kWvR0Tiles * 4;      // f32 [kRrMaxD]
+constexpr int kWvOffMisc = kWvOffQs + kRrMaxD * 4;        // u32 [8]
+constexpr int kWvLds = kWvOffMisc + 32;
+
+__device__ __forceinline__ void wave_rescore_any(uint64_t* keys, int m, const SelectArgs& a, const float* qs, int lane) {
+  const int cpl = ((a.rr_d >> 2) + 15) >> 4;
+  if (cpl <= 1) rescore_rows<1, 8, 4>(keys, m, a, qs, lane);
+  else if (cpl <= 2) rescore_rows<2, 8, 4>(keys, m, a, qs, lane);
+  else if (cpl <= 4) rescore_rows<4, 6, 4>(keys, m, a, qs, lane);
+  else if (cpl <= 6) rescore_rows<6, 5, 4>(keys, m, a, qs, lane);
+  else rescore_rows<8, 4, 4>(keys, m, a, qs, lane);
+}
+
+__global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
+  __shared__ __attribute__((aligned(16))) char dsm[kWvLds];
+  uint64_t* cand = (uint64_t*)(dsm + kWvOffCand);
+  uint32_t* tl = (uint32_t*)(dsm + kWvOffTl);
+  uint32_t* r0t = (uint32_t*)(dsm + kWvOffR0t);
+  float* qs = (float*)(dsm + kWvOffQs);
+  uint32_t* misc = (uint32_t*)(dsm + kWvOffMisc);
+  const int row = blockIdx.x, lane = threadIdx.x;
+  const int n = a.n_cols, K = a.K;
+  const int ntiles = (n + 31) >> 5;
+  const float* Srow = a.S + (size_t)row * a.lds;
+  auto s_quad = [&](int t, int g) -> float4 {
+    return a.s_blocked ? *(const float4*)(a.S + sblk_quad(row, t, g, a.ldt)) : *(const float4*)(Srow + t * 32 + 4 * g);
+  };
+  auto s_at = [&](int j) -> float {
+    return a.s_blocked ? a.S[sblk_quad(row, j >> 5, (j >> 2) & 7, a.ldt) + (j & 3)] : Srow[j];
+  };
+  const uint32_t* trow = a.tmax + (size_t)row * a.ldt;
+  const uint32_t* prow = a.max_inout ? a.pmax + (size_t)row * a.ldt : nullptr;
+  const uint32_t* excl = a.excl ? a.excl + (size_t)row * a.excl_ld : nullptr;
+  const int64_t w0 = a.slab_start >> 5;
+  auto elig = [&](int tile) -> uint32_t {
+    const uint32_t* pp = a.present ? a.present + w0 + tile : &kWordOnes;
+    const uint32_t* mp = a.mask ? a.mask + w0 + tile : &kWordOnes;
+    const uint32_t* ep = excl ? excl + w0 + tile : &kWordZero;
+    return *pp & *mp & ~*ep;
+  };
+  auto flag = [&]() {
+    if (lane == 0) a.rr_flags[row] = 1u;
+  };
+  auto stamp = [&](int slot) {  // probe-only phase timeline (s_memrealtime, 100 MHz)
+    if (a.trace && lane == 0) a.trace[row * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+
+  // ---- loads: maxima (and present maxima), the f32 query row, ε ----
+  uint32_t tm[kWvTPL], pm[kWvTPL];
+#pragma unroll
+  for (int j = 0; j < kWvTPL; ++j) {
+    const int t = lane + 64 * j;
+    tm[j] = t < ntiles ? trow[t] : 0u;
+    pm[j] = (prow && t < ntiles) ? prow[t] : 0u;
+  }
+  const int nq4 = a.rr_d >> 2;
+  float4 qv0 = make_float4(0.f, 0.f, 0.f, 0.f), qv1 = qv0;
+  const float4* qg = (const float4*)(a.rr_q + (size_t)row * a.rr_ld);
+  if (lane < nq4) qv0 = qg[lane];
+  if (lane + 64 < nq4) qv1 = qg[lane + 64];
+  const float eps2 = rr_margin(a.rr_eps[row]);
+  if (lane < nq4) ((float4*)qs)[lane] = qv0;
+  if (lane + 64 < nq4) ((float4*)qs)[lane + 64] = qv1;
+
+  // ---- bound: T0 = K-th largest tile maximum (0 maxima = no eligible item) ----
+  auto cnt_ge = [&](uint32_t c) -> uint32_t {
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kWvTPL; ++j) s += (uint32_t)__popcll(__ballot(tm[j] >= c));
+    return s;
+  };
+  uint32_t T0 = 1;  // fewer than K tiles with eligible items: every eligible item
+  if (cnt_ge(1u) >= (uint32_t)K) {
+    uint32_t hi = 0, lo = ~0u;
+#pragma unroll
+    for (int j = 0; j < kWvTPL; ++j) {
+      hi = max(hi, tm[j]);
+      lo = min(lo, tm[j] ? tm[j] : ~0u);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      const uint64_t y = __shfl_xor(best0, o);
-      best0 = y > best0 ? y : best0;
+      hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+      lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
     }
-    if (lane == 0) atomicMax((unsigned long long*)(misc + 10), (unsigned long long)best0);
-    __syncthreads();
-    if (tid == 0) a.max_inout[row] = *(const uint64_t*)(misc + 10);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    const uint32_t d = hi ^ lo;
+    const int top = d ? 31 - __builtin_clz(d) : -1;
+    uint32_t P = top < 0 ? hi : top >= 31 ? 0u : hi & ~((2u << top) - 1u);
+    for (int b = top; b >= 0; --b) {
+      const uint32_t c = P | (1u << b);
+      if (cnt_ge(c) >= (uint32_t)K) P = c;
+    }
+    T0 = P ? P : 1u;
   }
-  if (m == kRrSlow) {
-    rr_slow_path(a, row, n, a.rr_thr[2 * row], K, cand, misc, qs, elig, s_at);
-    return;
+  const uint32_t Tg = ord_sub(T0, eps2);
+  stamp(1);
+
+  // ---- qualifying tiles -> list ----
+  uint32_t ntl = 0;
+#pragma unroll
+  for (int j = 0; j < kWvTPL; ++j) {
+    const uint64_t qm = __ballot(tm[j] >= Tg && lane + 64 * j < ntiles);
+    const uint32_t pos = ntl + __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
+    if (((qm >> lane) & 1ull) && pos < (uint32_t)kWvTiles) tl[pos] = (uint32_t)(lane + 64 * j);
+    ntl += (uint32_t)__popcll(qm);
   }
-  rr_rescore_any(cand, (int)m, a, qs);
+  // rank 0: the present maximum (order image, lowest tile) and its margin
+  uint32_t Pm = 0, thr0 = 0, nt0 = 0;
+  if (prow) {
+#pragma unroll
+    for (int j = 0; j < kWvTPL; ++j) Pm = max(Pm, pm[j]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) Pm = max(Pm, (uint32_t)__shfl_xor((int)Pm, o));
+    Pm = __builtin_amdgcn_readfirstlane(Pm);
+    thr0 = ord_sub(Pm, eps2);
+    if (Pm) {
+#pragma unroll
+      for (int j = 0; j < kWvTPL; ++j) {
+        const uint64_t qm = __ballot(pm[j] >= thr0 && lane + 64 * j < ntiles);
+        const uint32_t pos = nt0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
+        if (((qm >> lane) & 1ull) && pos < (uint32_t)kWvR0Tiles) r0t[pos] = (uint32_t)(lane + 64 * j);
+        nt0 += (uint32_t)__popcll(qm);
+      }
+    }
+  }
+  if (ntl > (uint32_t)kWvTiles || nt0 > (uint32_t)kWvR0Tiles) return flag();
+  stamp(2);
+  if (lane == 0) misc[0] = 0u, misc[1] = 0u;
+  __syncthreads();  // (one wave: orders the LDS list writes before the reads below)
+
+  // ---- gather: eight lanes per qualifying tile (one 16-B score quad each, so a wave load
+  // reads eight whole 128-B tile rows), up to 128 tiles per round with every load issued
+  // before any is used ----
+  {
+    constexpr int kGP = 16;  // tiles per lane group per round
+    const int sub = lane & 7, grp = lane >> 3;
+    for (uint32_t base = 0; base < ntl; base += 8 * kGP) {
+      float4 v[kGP];
+      uint32_t okw[kGP];
+      int tt[kGP];
+#pragma unroll
+      for (int p = 0; p < kGP; ++p) {
+        const uint32_t i = base + 8 * p + grp;
+        tt[p] = i < ntl ? (int)tl[i] : -1;
+      }
+#pragma unroll
+      for (int p = 0; p < kGP; ++p) {
+        const int t = tt[p] < 0 ? (int)tl[0] : tt[p];
+        v[p] = s_quad(t, sub);
+        okw[p] = elig(t);
+      }
+#pragma unroll
+      for (int p = 0; p < kGP; ++p) {
+        const int t = tt[p];
+        const float f[4] = {v[p].x, v[p].y, v[p].z, v[p].w};
+        uint32_t m = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int it = 4 * sub + c;
+          m |= (t >= 0 && t * 32 + it < n && ((okw[p] >> it) & 1u) && ord_of(f[c]) >= Tg) ? (1u << c) : 0u;
+        }
+        if (m) {
+          uint32_t q = atomicAdd(&misc[0], (uint32_t)__popc(m));
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if ((m >> c) & 1u) {
+              if (q < (uint32_t)kWvCand) cand[q] = make_key(ord_of(f[c]), a.gid0 + (uint32_t)(t * 32 + 4 * sub + c));
+              ++q;
+            }
+        }
+      }
+    }
+  }
+  // rank-0 items: present, within the margin of the present maximum
+  uint64_t* r0k = cand + kWvCand;
+  for (uint32_t i = lane; i < nt0 * 32; i += 64) {
+    const int t = (int)r0t[i >> 5], it = (int)(i & 31), j = t * 32 + it;
+    const uint32_t pw = a.present ? a.present[w0 + t] : ~0u;
+    if (j < n && ((pw >> it) & 1u) && ord_of(s_at(j)) >= thr0) {
+      const uint32_t q = atomicAdd(&misc[1], 1u);
+      if (q < (uint32_t)kWvR0) r0k[q] = make_key(1u, a.gid0 + (uint32_t)j);
+    }
+  }
   __syncthreads();
-  const uint64_t gmax = *(const uint64_t*)(misc + 10);
-  if (wave != 0) return;
-  if (m <= 64) wave_sort_emit<1>(cand, (int)m, a, row, gmax);
-  else if (m <= 128) wave_sort_emit<2>(cand, (int)m, a, row, gmax);
-  else if (m <= 256) wave_sort_emit<4>(cand, (int)m, a, row, gmax);
-  else wave_sort_emit<8>(cand, (int)m, a, row, gmax);
+  const uint32_t cnt = __builtin_amdgcn_readfirstlane(misc[0]);
+  const uint32_t n0 = __builtin_amdgcn_readfirstlane(misc[1]);
+  if (cnt > (uint32_t)kWvCand || n0 > (uint32_t)kWvR0) return flag();
+  stamp(3);
+
+  // ---- rescore candidates and rank-0 items (rank-0 keys right behind the candidates) ----
+  for (uint32_t i = lane; i < n0; i += 64) cand[cnt + i] = r0k[i];
+  __syncthreads();
+  wave_rescore_any(cand, (int)(cnt + n0), a, qs, lane);
+  __syncthreads();
+  stamp(4);
+  uint64_t gmax = 0;
+  for (uint32_t i = lane; i < n0; i += 64) gmax = cand[cnt + i] > gmax ? cand[cnt + i] : gmax;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t y = __shfl_xor(gmax, o);
+    gmax = y > gmax ? y : gmax;
+  }
+  if (a.max_inout && lane == 0) a.max_inout[row] = gmax;
+  if (lane == 0) a.rr_flags[row] = 0u;
+  if (cnt <= 64) wave_sort_emit<1>(cand, (int)cnt, a, row, gmax);
+  else if (cnt <= 128) wave_sort_emit<2>(cand, (int)cnt, a, row, gmax);
+  else wave_sort_emit<4>(cand, (int)cnt, a, row, gmax);
+  stamp(5);
+  if (a.trace && lane == 0) a.trace[row * 8 + 6] = cnt, a.trace[row * 8 + 7] = ntl;
+}
+
+hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s) {
+  if (!a.rr_eps || !a.rr_x || !a.rr_q || !a.rr_flags || a.rr_out || a.carry_in || a.rr_d <= 0 || a.rr_d > kRrMaxD ||
+      (a.rr_d & 3) || a.K <= 0 || a.K > kWvCand || B <= 0 || a.n_cols <= 0 || a.n_cols > 64 * kWvTPL * 32 || !a.tmax ||
+      (a.max_inout && !a.pmax) || (a.slab_start & 31) || (a.out_scores && a.k_final > kWvCand))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(select_rr_wave_kernel, dim3(B), dim3(64), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_rerank(const SelectArgs& a, int B, hipStream_t s) {
@@ -1149,6 +1471,14 @@ hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s) {
   if (a.K <= 0 || a.K > kMaxKInt || B <= 0 || a.n_cols <= 0 || !a.tmax || (a.max_inout && !a.pmax) ||
       (a.slab_start & 31))
     return hipErrorInvalidValue;
+  // re-rank (rr_eps set): operands always; the hand-off buffers only for the split launch
+  if (a.rr_eps && (!a.rr_x || !a.rr_q || a.rr_d <= 0 || a.rr_d > kRrMaxD || (a.rr_d & 3) || a.rr_d > 4 * kSelectThreads ||
+                   (a.rr_out && (!a.rr_cnt || !a.rr_thr || (a.max_inout && (!a.rr_r0 || !a.rr_r0n))))))
+    return hipErrorInvalidValue;
+  if (a.rr_eps) {
+    hipLaunchKernelGGL((select_kernel<0, true>), dim3(B), dim3(kSelectThreads), 0, s, a);
+    return hipGetLastError();
+  }
   static const int abl = getenv("BB_SELECT_ABLATE") ? atoi(getenv("BB_SELECT_ABLATE")) : 0;
   switch (abl) {
     case 1: hipLaunchKernelGGL(select_kernel<1>, dim3(B), dim3(kSelectThreads), 0, s, a); break;

@@ -62,7 +62,8 @@ def test_rr_configs1_shape_bit_exact(brickrec):
     idx.set_profiling(True)
     sc, ids, cnt = idx.search("semantic", k, q_rows=q)
     prof = idx.profile()
-    assert prof["gemm"]["launches"] == 1 and prof["select"]["launches"] == 1, prof
+    # one scan; the one-wave select plus the block select of the rows it leaves (if any)
+    assert prof["gemm"]["launches"] == 1 and prof["select"]["launches"] in (1, 2), prof
     rows = idx.get_rows(np.arange(n))
     qo = _qop(q)
     for i in range(0, B, 4):
@@ -138,6 +139,45 @@ def test_rr_cf_and_hybrid_sides_exact(brickrec):
     for i in range(0, B, 5):
         ci, cs = _exact_topk(rows, rows[qi[i]], 2 * k, drop_rank0_present=np.ones(n, bool))
         fi, fs = _exact_topk(f, u[i], 2 * k, ~excl[i])
+        bi, bs = R.union_blend(ci, cs.astype(np.float64), fi, fs.astype(np.float64), 0.4, 0.6, k)
+        assert list(hid[i][: len(bi)]) == list(bi)
+        np.testing.assert_allclose(hs[i][: len(bi)], bs, atol=1e-6, rtol=0)
+
+
+def test_rr_wave_select_mixed_batch(brickrec):
+    """Query chunks > 256 rows take the one-wave select; rows that overflow its caps (queries
+    inside a cluster of near-duplicates) are handed to the block select in the same search.
+    Semantic, similar-sets (rank 0) with a mask, and the hybrid sides, all bit-exact."""
+    rng = np.random.default_rng(12)
+    n, d, r, k = 25216, 384, 50, 50
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    v = rng.standard_normal(d).astype(np.float32)
+    dup = rng.choice(n, 1500, replace=False)
+    x[dup] = v + 3e-3 * rng.standard_normal((1500, d)).astype(np.float32)
+    mask = rng.random(n) < 0.6
+    B = 600
+    q = rng.standard_normal((B, d)).astype(np.float32)
+    q[::50] = v + 1e-3 * rng.standard_normal((len(q[::50]), d)).astype(np.float32)  # 12 cluster queries
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(x)
+    rows = idx.get_rows(np.arange(n))
+    qo = _qop(q)
+    sc, ids, cnt = idx.search("semantic", k, q_rows=q)
+    for i in list(range(0, B, 50)) + list(range(7, B, 37)):
+        ri, rs = _exact_topk(rows, qo[i], k)
+        _assert_exact(sc[i], ids[i], ri, rs)
+    qi = np.concatenate([dup[:8], rng.choice(n, 292, replace=False)])
+    sc, ids, cnt = idx.search("similar", k, q_items=qi, mask=mask)
+    for j in list(range(8)) + list(range(8, 300, 23)):
+        ri, rs = _exact_topk(rows, rows[qi[j]], k, mask, drop_rank0_present=np.ones(n, bool))
+        _assert_exact(sc[j], ids[j], ri, rs)
+    f = rng.normal(0, 0.1, (n, r)).astype(np.float32)
+    u = rng.normal(0, 0.1, (300, r)).astype(np.float32)
+    idx.upload_cf(f)
+    hs, hid, hc = idx.search("hybrid", k, q_items=qi, q_cf=u)
+    for i in list(range(0, 8, 3)) + list(range(8, 300, 41)):
+        ci, cs = _exact_topk(rows, rows[qi[i]], 2 * k, drop_rank0_present=np.ones(n, bool))
+        fi, fs = _exact_topk(f, u[i], 2 * k)
         bi, bs = R.union_blend(ci, cs.astype(np.float64), fi, fs.astype(np.float64), 0.4, 0.6, k)
         assert list(hid[i][: len(bi)]) == list(bi)
         np.testing.assert_allclose(hs[i][: len(bi)], bs, atol=1e-6, rtol=0)
