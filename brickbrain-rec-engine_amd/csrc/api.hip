@@ -612,9 +612,13 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   if (need_cf && (rc = x->qcf.ensure(std::max((size_t)Bc * x->Rpad * qes_f, (size_t)Bc * x->Rpad_b * 2)))) return rc;
   if (rr_c && ((rc = x->qf32.ensure((size_t)Bc * x->Dpad * 4)) || (rc = x->qeps.ensure((size_t)Bc * 4)))) return rc;
   if (rr_f && ((rc = x->qcf32.ensure((size_t)Bc * x->Rpad * 4)) || (rc = x->qcfeps.ensure((size_t)Bc * 4)))) return rc;
-  // the select kernel rescores its candidates itself; BB_RR_SPLIT (A/B runs) hands them to
-  // a separate rerank_kernel launch instead
-  static const bool rr_split = getenv("BB_RR_SPLIT") != nullptr;
+  // The block select hands its candidates to a separate rerank_kernel launch; BB_RR_FUSED=1
+  // makes the select kernel rescore them itself.  Measured on one box (r02zd, configs[1]):
+  // fused serial p50 52.6 us vs 55.5 us split, but with three batches in flight split
+  // 8.30 M q/s vs fused 7.66 M q/s — two shorter launches leave the CUs to the next batch's
+  // scan sooner than one long one.  (The one-wave select of query chunks > 256 rows always
+  // rescores in place.)
+  static const bool rr_split = !(getenv("BB_RR_FUSED") && atoi(getenv("BB_RR_FUSED")) == 1);
   if ((rr_c || rr_f) && rr_split &&
       ((rc = x->rr_out.ensure((size_t)Bc * kRrCap * 8)) || (rc = x->rr_cnt.ensure((size_t)Bc * 4)) ||
        (rc = x->rr_thr.ensure((size_t)Bc * 8)) || (rc = x->rr_r0.ensure((size_t)Bc * kRrR0Cap * 4)) ||
@@ -935,13 +939,6 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           sa.rr_ld = cf_side ? x->Rpad : x->Dpad;
           sa.rr_d = (int)sa.rr_ld;
           sa.rr_gid_base = (uint32_t)x->id_offset;
-          if (rr_split) {  // (A/B) hand-off buffers: a separate rerank_kernel launch finishes
-            sa.rr_out = (uint64_t*)x->rr_out.p;
-            sa.rr_cnt = (uint32_t*)x->rr_cnt.p;
-            sa.rr_thr = (uint32_t*)x->rr_thr.p;
-            sa.rr_r0 = (uint32_t*)x->rr_r0.p;
-            sa.rr_r0n = (uint32_t*)x->rr_r0n.p;
-          }
         }
         sa.carry_in = sl && !stream ? keys + ((size_t)(pp ^ 1) * sides + side) * side_keys : nullptr;
         sa.keys_out = pilot ? (uint64_t*)x->pilot.p : keys + ((size_t)pp * sides + side) * side_keys;
@@ -968,9 +965,18 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         // flight; at B <= 256 the block select's four waves per query win on latency (19 vs
         // 34 us per query).  BB_SELECT_WAVE=0/1 (A/B runs) forces it off / on.
         static const int sel_wave_env = getenv("BB_SELECT_WAVE") ? atoi(getenv("BB_SELECT_WAVE")) : -1;
-        const bool sel_wave = rr_side && !rr_split && !sa.carry_in && ncols <= 32768 && K_int <= 256 &&
+        const bool sel_wave = rr_side && !sa.carry_in && ncols <= 32768 && K_int <= 256 &&
                               (!sa.out_scores || q->k <= 256) &&
                               (sel_wave_env == 1 || (sel_wave_env != 0 && bc > 256));
+        // block select of a re-rank search: hand-off buffers for the rerank_kernel launch
+        const bool rr_handoff = rr_side && rr_split && !sel_wave;
+        if (rr_handoff) {
+          sa.rr_out = (uint64_t*)x->rr_out.p;
+          sa.rr_cnt = (uint32_t*)x->rr_cnt.p;
+          sa.rr_thr = (uint32_t*)x->rr_thr.p;
+          sa.rr_r0 = (uint32_t*)x->rr_r0.p;
+          sa.rr_r0n = (uint32_t*)x->rr_r0n.p;
+        }
         if (sel_wave) {
           if ((rc = x->rr_flags.ensure((size_t)Bc * 4))) return rc;
           sa.rr_flags = (uint32_t*)x->rr_flags.p;
@@ -1016,7 +1022,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
                   acc[3] / bc / 100, acc[4] / bc / 100, acc[5] / bc / 100, acc[6] / bc / 100, acc[7] / bc / 100,
                   (double)(t1 - t0) / 100);
         }
-        if (rr_side && rr_split && (rc = timed(x, K_RERANK, s, [&] { return launch_rerank(sa, bc, s); }))) return rc;
+        if (rr_handoff && (rc = timed(x, K_RERANK, s, [&] { return launch_rerank(sa, bc, s); }))) return rc;
         final_pp = pp;
       }
     }

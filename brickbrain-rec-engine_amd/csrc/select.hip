@@ -323,18 +323,18 @@ __device__ __forceinline__ double sum16_f64(double v) {
 __device__ __forceinline__ uint64_t rr_key(float e, uint32_t gid) { return make_key(ord_of(e + 0.0f), gid); }
 
 // Rescore keys[0..m) in place (approximate / placeholder -> exact keys).  NG lane groups of
-// 16 (NG·16 threads call it together), U rows per group in flight; the lane's query chunks
-// are held in f64.
+// 16 (NG·16 threads call it together), U rows per group in flight (U·CPL <= 12 chunks per
+// lane: the select's register budget, not its row latency, bounds the in-flight throughput —
+// a fat select wave keeps the next batch's scan off the CU).
 template <int CPL, int U, int NG>
 __device__ __forceinline__ void rescore_rows(uint64_t* keys, int m, const SelectArgs& a, const float* qs, int t) {
   const int p = t & 15, g = t >> 4;
   const int nch = a.rr_d >> 2;
-  double qd[CPL][4];
+  f4v qv[CPL];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
     const int c = p + 16 * j;
-    const f4v v = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
-    qd[j][0] = v.x, qd[j][1] = v.y, qd[j][2] = v.z, qd[j][3] = v.w;
+    qv[j] = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
   }
   for (int c0 = g * U; c0 < m; c0 += NG * U) {
     uint32_t gid[U];
@@ -352,25 +352,25 @@ __device__ __forceinline__ void rescore_rows(uint64_t* keys, int m, const Select
 #pragma unroll
       for (int j = 0; j < CPL; ++j)
         if (p + 16 * j < nch) {
-          acc = fma((double)xv[u][j].x, qd[j][0], acc);
-          acc = fma((double)xv[u][j].y, qd[j][1], acc);
-          acc = fma((double)xv[u][j].z, qd[j][2], acc);
-          acc = fma((double)xv[u][j].w, qd[j][3], acc);
+          acc = fma((double)xv[u][j].x, (double)qv[j].x, acc);
+          acc = fma((double)xv[u][j].y, (double)qv[j].y, acc);
+          acc = fma((double)xv[u][j].z, (double)qv[j].z, acc);
+          acc = fma((double)xv[u][j].w, (double)qv[j].w, acc);
         }
       acc = sum16_f64(acc);
       if (p == 0 && c0 + u < m) keys[c0 + u] = rr_key((float)acc, gid[u]);
     }
   }
 }
-// block select (256 threads): one round for up to 96 rows at d <= 384
+// block select (256 threads)
 __device__ __forceinline__ void rr_rescore_any(uint64_t* keys, int m, const SelectArgs& a, const float* qs) {
   const int cpl = ((a.rr_d >> 2) + 15) >> 4;
   const int t = threadIdx.x;
-  if (cpl <= 1) rescore_rows<1, 8, 16>(keys, m, a, qs, t);
-  else if (cpl <= 2) rescore_rows<2, 8, 16>(keys, m, a, qs, t);
-  else if (cpl <= 4) rescore_rows<4, 6, 16>(keys, m, a, qs, t);
-  else if (cpl <= 6) rescore_rows<6, 6, 16>(keys, m, a, qs, t);
-  else rescore_rows<8, 4, 16>(keys, m, a, qs, t);   // rows up to kRrMaxD = 512 wide
+  if (cpl <= 1) rescore_rows<1, 12, 16>(keys, m, a, qs, t);
+  else if (cpl <= 2) rescore_rows<2, 6, 16>(keys, m, a, qs, t);
+  else if (cpl <= 4) rescore_rows<4, 3, 16>(keys, m, a, qs, t);
+  else if (cpl <= 6) rescore_rows<6, 2, 16>(keys, m, a, qs, t);
+  else rescore_rows<8, 1, 16>(keys, m, a, qs, t);   // rows up to kRrMaxD = 512 wide
 }
 
 // Re-rank with masses of items at the gather bound (more than kCandCap): an exact running
@@ -1235,11 +1235,11 @@ constexpr int kWvLds = kWvOffMisc + 32;
 
 __device__ __forceinline__ void wave_rescore_any(uint64_t* keys, int m, const SelectArgs& a, const float* qs, int lane) {
   const int cpl = ((a.rr_d >> 2) + 15) >> 4;
-  if (cpl <= 1) rescore_rows<1, 8, 4>(keys, m, a, qs, lane);
-  else if (cpl <= 2) rescore_rows<2, 8, 4>(keys, m, a, qs, lane);
-  else if (cpl <= 4) rescore_rows<4, 6, 4>(keys, m, a, qs, lane);
-  else if (cpl <= 6) rescore_rows<6, 5, 4>(keys, m, a, qs, lane);
-  else rescore_rows<8, 4, 4>(keys, m, a, qs, lane);
+  if (cpl <= 1) rescore_rows<1, 12, 4>(keys, m, a, qs, lane);
+  else if (cpl <= 2) rescore_rows<2, 6, 4>(keys, m, a, qs, lane);
+  else if (cpl <= 4) rescore_rows<4, 3, 4>(keys, m, a, qs, lane);
+  else if (cpl <= 6) rescore_rows<6, 2, 4>(keys, m, a, qs, lane);
+  else rescore_rows<8, 1, 4>(keys, m, a, qs, lane);
 }
 
 __global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {

@@ -181,3 +181,36 @@ def test_rr_wave_select_mixed_batch(brickrec):
         bi, bs = R.union_blend(ci, cs.astype(np.float64), fi, fs.astype(np.float64), 0.4, 0.6, k)
         assert list(hid[i][: len(bi)]) == list(bi)
         np.testing.assert_allclose(hs[i][: len(bi)], bs, atol=1e-6, rtol=0)
+
+
+def test_rr_fused_select_variant():
+    """BB_RR_FUSED=1 (select kernel rescores in place, no rerank launch) gives the same bits as
+    the default split launch; the variant is chosen once per process, so it runs in a child."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import brickrec
+from oracle import restatement as R
+n, d, B, k = 25216, 384, 256, 50
+x = R.unit_rows(n, d, 1234); q = R.unit_rows(B, d, 4321)
+idx = brickrec.ItemIndex(dtype="f32"); idx.upload_items(x)
+sc, ids, _ = idx.search("semantic", k, q_rows=q)
+rows = idx.get_rows(np.arange(n)); rng = np.random.default_rng(3)
+qi = rng.choice(n, 64, replace=False); m = rng.random(n) < 0.5
+s2, i2, _ = idx.search("similar", k, q_items=qi, mask=m)
+np.savez(sys.argv[3], sc=sc, ids=ids, s2=s2, i2=i2)
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "brickbrain-rec-engine_amd")
+    out = {}
+    for fused in ("0", "1"):
+        path = os.path.join(root, "gpurun_out", f"rr_fused_{fused}.npz")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        env = dict(os.environ, BB_RR_FUSED=fused)
+        subprocess.run([sys.executable, "-c", code, root, pkg, path], check=True, env=env, timeout=120)
+        out[fused] = np.load(path)
+    for key in ("sc", "ids", "s2", "i2"):
+        assert np.array_equal(out["0"][key], out["1"][key]), key
