@@ -124,6 +124,15 @@ __host__ __device__ inline size_t sblk_quad(int q, int t, int g, int64_t ldt) {
   return (((size_t)(q >> 5) * ldt + t) * 4 + (g >> 1)) * 256 + (((g & 1) << 5) | (q & 31)) * 4;
 }
 
+// XCD-aware bijection blockIdx -> row of [0, total): workgroup L runs on XCD L & 7, and each
+// XCD takes one contiguous run of rows.  Rows that share cache lines (the 32 queries of a
+// blocked score image block, sblk_quad) then share that XCD's L2 instead of fetching every
+// line into eight L2s.
+__device__ __forceinline__ int xcd_row(int L, int total) {
+  const int xcd = L & 7, local = L >> 3, q8 = total >> 3, r8 = total & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+}
+
 struct SelectArgs {
   const float* S;           // scores [B][lds]
   int64_t lds;

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   uint32_t* scan_sh = misc + 16;                  // 8 words
   uint64_t* red = (uint64_t*)(misc + 32);         // 4 u64
 
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = xcd_row(blockIdx.x, gridDim.x), tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (RR && a.rr_flags && a.rr_flags[row] == 0u) return;  // finished by select_rr_wave_kernel
   const int n = a.n_cols, K = a.K;
   const int ntiles = (n + 31) >> 5;
@@ -945,7 +945,7 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
   uint32_t* misc = (uint32_t*)(dsm + kCsOffMisc);
   uint32_t* scan_sh = misc + 16;
   uint64_t* red = (uint64_t*)(misc + 32);
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = xcd_row(blockIdx.x, gridDim.x), tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int R = a.regions;
   const size_t rbase = (size_t)row * R;
 
@@ -1176,7 +1176,7 @@ __global__ __launch_bounds__(kSelectThreads) void rerank_kernel(SelectArgs a) {
   uint64_t* cand = (uint64_t*)dsm;
   float* qs = (float*)(dsm + kRrOffQ);
   uint32_t* misc = (uint32_t*)(dsm + kRrOffMisc);
-  const int row = blockIdx.x, tid = threadIdx.x;
+  const int row = xcd_row(blockIdx.x, gridDim.x), tid = threadIdx.x;
   const int n = a.n_cols;
   const float* Srow = a.S + (size_t)row * a.lds;
   auto s_at = [&](int j) -> float {
@@ -1233,15 +1233,21 @@ constexpr int kWvOffQs = kWvOffR0t + kWvR0Tiles * 4;      // f32 [kRrMaxD]
 constexpr int kWvOffMisc = kWvOffQs + kRrMaxD * 4;        // u32 [8]
 constexpr int kWvLds = kWvOffMisc + 32;
 
+// UM: rows in flight per lane group, as a multiple of the block select's budget.  The
+// rescore is a chain of dependent row gathers (~1 us each from the MALL), so with one query
+// wave per SIMD (B <= ~1K) more rows per round pay; with several waves per SIMD the extra
+// registers cost occupancy instead (launch_select_rr_wave picks).
+template <int UM>
 __device__ __forceinline__ void wave_rescore_any(uint64_t* keys, int m, const SelectArgs& a, const float* qs, int lane) {
   const int cpl = ((a.rr_d >> 2) + 15) >> 4;
-  if (cpl <= 1) rescore_rows<1, 12, 4>(keys, m, a, qs, lane);
-  else if (cpl <= 2) rescore_rows<2, 6, 4>(keys, m, a, qs, lane);
-  else if (cpl <= 4) rescore_rows<4, 3, 4>(keys, m, a, qs, lane);
-  else if (cpl <= 6) rescore_rows<6, 2, 4>(keys, m, a, qs, lane);
-  else rescore_rows<8, 1, 4>(keys, m, a, qs, lane);
+  if (cpl <= 1) rescore_rows<1, 12 * UM, 4>(keys, m, a, qs, lane);
+  else if (cpl <= 2) rescore_rows<2, 6 * UM, 4>(keys, m, a, qs, lane);
+  else if (cpl <= 4) rescore_rows<4, 3 * UM, 4>(keys, m, a, qs, lane);
+  else if (cpl <= 6) rescore_rows<6, 2 * UM, 4>(keys, m, a, qs, lane);
+  else rescore_rows<8, 1 * UM, 4>(keys, m, a, qs, lane);
 }
 
+template <int UM>
 __global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
   __shared__ __attribute__((aligned(16))) char dsm[kWvLds];
   uint64_t* cand = (uint64_t*)(dsm + kWvOffCand);
@@ -1249,7 +1255,7 @@ __global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
   uint32_t* r0t = (uint32_t*)(dsm + kWvOffR0t);
   float* qs = (float*)(dsm + kWvOffQs);
   uint32_t* misc = (uint32_t*)(dsm + kWvOffMisc);
-  const int row = blockIdx.x, lane = threadIdx.x;
+  const int row = xcd_row(blockIdx.x, gridDim.x), lane = threadIdx.x;
   const int n = a.n_cols, K = a.K;
   const int ntiles = (n + 31) >> 5;
   const float* Srow = a.S + (size_t)row * a.lds;
@@ -1423,7 +1429,7 @@ __global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
   // ---- rescore candidates and rank-0 items (rank-0 keys right behind the candidates) ----
   for (uint32_t i = lane; i < n0; i += 64) cand[cnt + i] = r0k[i];
   __syncthreads();
-  wave_rescore_any(cand, (int)(cnt + n0), a, qs, lane);
+  wave_rescore_any<UM>(cand, (int)(cnt + n0), a, qs, lane);
   __syncthreads();
   stamp(4);
   uint64_t gmax = 0;
@@ -1447,7 +1453,13 @@ hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s) {
       (a.rr_d & 3) || a.K <= 0 || a.K > kWvCand || B <= 0 || a.n_cols <= 0 || a.n_cols > 64 * kWvTPL * 32 || !a.tmax ||
       (a.max_inout && !a.pmax) || (a.slab_start & 31) || (a.out_scores && a.k_final > kWvCand))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(select_rr_wave_kernel, dim3(B), dim3(64), 0, s, a);
+  // two waves per SIMD at most for the fat variant: 256 CUs x 4 SIMDs x 2
+  static const int um_env = getenv("BB_WAVE_UM") ? atoi(getenv("BB_WAVE_UM")) : 0;
+  const bool fat = um_env ? um_env == 2 : true;
+  if (fat)
+    hipLaunchKernelGGL(select_rr_wave_kernel<2>, dim3(B), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(select_rr_wave_kernel<1>, dim3(B), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 
