@@ -106,6 +106,7 @@ struct bb_index {
   // workspace
   DevBuf qn, qcf, S, tmax, keys, maxk, stage_in, out_sc, out_id, out_cnt, tmp;
   DevBuf qf32, qeps, qcf32, qcfeps;  // re-rank: f32 query rows and per-query bounds
+  DevBuf qh, qcfh;                   // re-rank: per-query quanta of the int16 score image
   DevBuf rr_out, rr_cnt, rr_thr, rr_r0, rr_r0n;  // re-rank: select -> rerank hand-off
   // streaming top-K (large indexes): pilot lists, candidate regions, overflow flag
   DevBuf pilot, cand, cand_cnt, cand_pmax, ovf;
@@ -270,7 +271,7 @@ int bb_destroy(bb_index* x) {
     for (DevBuf* b : {&x->items, &x->items_present, &x->ones, &x->zeros, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S, &x->tmax,
                       &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
                       &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
-                      &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->rr_out, &x->rr_cnt,
+                      &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
                       &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
@@ -610,8 +611,16 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   const size_t qes_c = x->items3.p ? std::max<size_t>(es, 6) : es, qes_f = x->cf3.p ? std::max<size_t>(es, 6) : es;
   if (need_content && (rc = x->qn.ensure(std::max((size_t)Bc * x->Dpad * qes_c, (size_t)Bc * x->Dpad_b * 2)))) return rc;
   if (need_cf && (rc = x->qcf.ensure(std::max((size_t)Bc * x->Rpad * qes_f, (size_t)Bc * x->Rpad_b * 2)))) return rc;
-  if (rr_c && ((rc = x->qf32.ensure((size_t)Bc * x->Dpad * 4)) || (rc = x->qeps.ensure((size_t)Bc * 4)))) return rc;
-  if (rr_f && ((rc = x->qcf32.ensure((size_t)Bc * x->Rpad * 4)) || (rc = x->qcfeps.ensure((size_t)Bc * 4)))) return rc;
+  if (rr_c && ((rc = x->qf32.ensure((size_t)Bc * x->Dpad * 4)) || (rc = x->qeps.ensure((size_t)Bc * 4)) ||
+               (rc = x->qh.ensure((size_t)Bc * 4))))
+    return rc;
+  if (rr_f && ((rc = x->qcf32.ensure((size_t)Bc * x->Rpad * 4)) || (rc = x->qcfeps.ensure((size_t)Bc * 4)) ||
+               (rc = x->qcfh.ensure((size_t)Bc * 4))))
+    return rc;
+  // re-rank scans write an int16 score image (2 B per score: half the slab traffic of f32;
+  // the quantum is folded into ε, common.h rr_quantum).  BB_S16=0 (A/B runs) keeps f32.
+  // BB_S16: 0 off, 1 every re-rank scan, 2 only scan4 (query chunks > 256 rows)
+  static const int s16_env = getenv("BB_S16") ? atoi(getenv("BB_S16")) : 1;
   // The block select hands its candidates to a separate rerank_kernel launch; BB_RR_FUSED=1
   // makes the select kernel rescore them itself.  Measured on one box (r02zd, configs[1]):
   // fused serial p50 52.6 us vs 55.5 us split, but with three batches in flight split
@@ -728,6 +737,11 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
                           (gather_c || (q->q_dtype == F32 && x->d % 4 == 0 && rows_c && ((uintptr_t)rows_c & 15) == 0));
     const bool rrfuse_f = rr_fuse_prep && !no_fuse && rr_f && !scan4_used(BF16, bpad) && q->q_cf_dtype == F32 && x->r % 4 == 0 &&
                           rows_f && ((uintptr_t)rows_f & 15) == 0;
+    // int16 score image on the re-rank scans (not with the fused re-rank prologue, whose
+    // chunk-0 workgroups write the bound while the others already store scores)
+    const bool s16_on = s16_env == 1 || (s16_env == 2 && scan4_used(BF16, bpad));
+    const bool s16_c = s16_on && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
+    const bool s16_f = s16_on && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
     if (need_content && !fuse_c && !rrfuse_c) {
       PrepArgs pa{};
       pa.Bpad = bpad;
@@ -743,6 +757,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         pa.Dpad_f = x->Dpad;
         pa.eps_out = (float*)x->qeps.p;
         pa.istats = (const float*)x->rr_stats.p;
+        pa.h_out = s16_c ? (float*)x->qh.p : nullptr;
       }
       pa.items = x->items.p;
       pa.n_items = x->n;
@@ -772,6 +787,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         pa.Dpad_f = x->Rpad;
         pa.eps_out = (float*)x->qcfeps.p;
         pa.istats = (const float*)x->rr_stats.p + 4;
+        pa.h_out = s16_f ? (float*)x->qcfh.p : nullptr;
       }
       pa.src = (const char*)d_cf + (size_t)b0 * x->r * es_cf;
       pa.src_dtype = q->q_cf_dtype;
@@ -870,6 +886,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           ga.X = (const char*)(cf_side ? x->cf_bf.p : x->items_bf.p) + (size_t)c0 * w * 2;
           ga.ldx = ga.ldq = w;
           ga.Kpad = (int)w;
+          ga.s_h = (cf_side ? s16_f : s16_c) ? (const float*)(cf_side ? x->qcfh.p : x->qh.p) : nullptr;
           if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(BF16, ga, s); }))) return rc;
         } else if (cf_side ? s3_f : s3_c) {
           // split-precision scan: items, gathered rows and prepped queries are bf16 planes
@@ -929,11 +946,13 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         sa.excl_ld = nw;
         sa.K = K_int;
         // blocked score image: the split scan, and the bf16 scan with 64 queries per wave
-        sa.s_blocked = ((cf_side ? s3_f : s3_c) ||
-                        ((cf_side ? scan_f : scan_c) && scan4_used(x->dtype, bpad)) ||
-                        (rr_side && scan4_used(BF16, bpad))) ? 1 : 0;
+        // every scan kernel (scan2 / scan3 / scan4) writes the blocked image; the tiled
+        // gemm_nt fallback writes row-major S
+        sa.s_blocked = ((cf_side ? s3_f : s3_c) || (cf_side ? scan_f : scan_c) ||
+                        (rr_side && gemm_uses_scan(BF16, bpad, cf_side ? x->Rpad_b : x->Dpad_b))) ? 1 : 0;
         if (rr_side) {
           sa.rr_eps = (const float*)(cf_side ? x->qcfeps.p : x->qeps.p);
+          sa.s_h = (cf_side ? s16_f : s16_c) ? (const float*)(cf_side ? x->qcfh.p : x->qh.p) : nullptr;
           sa.rr_x = (const float*)(cf_side ? x->cf.p : x->items.p);
           sa.rr_q = (const float*)(cf_side ? x->qcf32.p : x->qf32.p);
           sa.rr_ld = cf_side ? x->Rpad : x->Dpad;

@@ -86,8 +86,35 @@ struct GemmArgs {
   uint64_t* cand_pmax;      // [Mpad·n_chunks·2] rank-0 key per region (present max) or null
   int32_t cand_cap;
   uint32_t gid0;            // global id of column 0
+  // int16 score image (scan ABL & kScanS16, exact re-rank path): score s of query q is stored
+  // as the code c = round(s / s_h[q]) (saturating, never reached: see rr_quantum), so the
+  // slab costs 2 B per score; the select decodes c·s_h[q], whose bound ε (prep) covers it
+  const float* s_h;         // [Mpad] quantum per query row
+  float* q_h_out;           // fused re-rank prologue: writes the quantum beside q_eps_out
 };
 constexpr int kScanStream = 512;  // scan ABL bit: streaming top-K epilogue
+constexpr int kScanS16 = 4096;    // scan ABL bit: int16 score image (GemmArgs.s_h)
+
+// Quantum h of the int16 score image of one query and the widened bound of its decoded
+// scores.  |approximate score| <= |q̃|·Ñ_x·(1+γ) <= 16384·h, so no code saturates; the
+// encode (v_cvt_pknorm_i16_f32 of s·(1/(h·32767)), whatever its rounding) and the f32
+// decode c·h move a score by at most h·(1 + 2^-8): ε' = (ε + 1.01·h)(1 + 2^-20) bounds
+// |decoded − exact| wherever ε bounded |approximate − exact|.  h = ε/8 keeps the re-rank
+// window within ~13 % of its f32-slab width.
+__device__ inline void rr_quantum(double eps, double qnorm, double nx, float& eps_out, float& h_out) {
+  double h = eps / 8.0;
+  const double floor_h = 0x1p-14 * qnorm * nx * (1.0 + 0x1p-10);
+  if (h < floor_h) h = floor_h;
+  h_out = __double2float_ru(h);
+  eps_out = __double2float_ru((eps + 1.01 * (double)h_out) * (1.0 + 0x1p-20));
+}
+
+// Two scores -> two int16 codes of the score image (quantum 1/(k·32767)).
+__device__ __forceinline__ uint32_t s16_pack(float x, float y, float k) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_i16(x * k, y * k));
+}
+__device__ __forceinline__ float s16_lo(uint32_t w, float h) { return (float)(int16_t)(w & 0xFFFFu) * h; }
+__device__ __forceinline__ float s16_hi(uint32_t w, float h) { return (float)(int16_t)(w >> 16) * h; }
 
 // Item chunks of a query-resident scan launch (shared by the launcher and the host code
 // sizing the streaming candidate regions): one workgroup per CU, ~256 workgroups.
@@ -178,6 +205,8 @@ struct SelectArgs {
   // one-wave re-rank select (select_rr_wave_kernel): 1 = the row overflowed a cap and is left
   // to the block select, which then skips every row whose flag is 0
   uint32_t* rr_flags;       // [B] or null
+  // int16 score image (GemmArgs.s_h): S holds codes, score = code · s_h[row]; null = f32 S
+  const float* s_h;
 };
 constexpr int kRrCap = 512;
 constexpr int kRrR0Cap = 64;
@@ -238,6 +267,7 @@ struct PrepArgs {
   int32_t Dpad_f;
   float* eps_out;           // [Bpad]
   const float* istats;      // [3]: max |x̃−x|, max |x|, max |x̃| over the item rows
+  float* h_out;             // [Bpad] int16 score-image quantum (rr_quantum; eps_out widened), or null
 };
 
 struct MaskArgs {

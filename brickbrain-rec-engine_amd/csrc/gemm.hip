@@ -56,13 +56,16 @@ static void launch_scan_t(const GemmArgs& a, hipStream_t s) {
   const int tiles = a.Ncols / 32;
   // one workgroup per CU (LDS + VGPR budget): ~256 workgroups, chunks balanced to ±1 tile
   const int n_chunks = scan_n_chunks(a.Mpad, tiles);
-  static const bool v1 = getenv("BB_SCAN_V1") != nullptr;
+  if constexpr (sizeof(T) == 2 && KU <= kRrMaxD / 8) {
+    if (a.s_h && !a.cand) {  // exact re-rank path: int16 score image
+      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanS16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
+                         n_chunks, tiles);
+      return;
+    }
+  }
   if (a.cand)
     hipLaunchKernelGGL((scan2_kernel<T, KU, kScanStream>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
                        n_chunks, tiles);
-  else if (v1 && !a.q_ids && !a.q_src)
-    hipLaunchKernelGGL((scan_kernel<T, KU>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks,
-                       tiles);
   else
     hipLaunchKernelGGL((scan2_kernel<T, KU>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks,
                        tiles);
@@ -132,6 +135,9 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   // the fused re-rank prologue lives in scan2 (bf16, query chunks of <= 128 rows) only
   if (a.q_istats && (dtype != BF16 || scan4_used(BF16, a.Mpad) || !a.q_f32_out || !a.q_eps_out || a.cand))
+    return hipErrorInvalidValue;
+  // the int16 score image: bf16 scans of rows up to kRrMaxD, slab epilogue only
+  if (a.s_h && (dtype != BF16 || a.cand || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.Kpad > kRrMaxD))
     return hipErrorInvalidValue;
   if (gemm_uses_scan(dtype, a.Mpad, a.Kpad)) {
     if (dtype == BF16 ? launch_scan<uint16_t>(a, s) : launch_scan<float>(a, s)) return hipGetLastError();

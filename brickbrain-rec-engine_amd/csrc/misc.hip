@@ -232,7 +232,11 @@ struct RrAcc {
     if (lane == 0) {
       const double gam = 2.0 * (double)a.Dpad * 0x1p-24;
       const double eps = (double)a.istats[0] * b + (double)a.istats[1] * e + gam * (double)a.istats[2] * b;
-      a.eps_out[row] = __double2float_ru(eps * (1.0 + 0x1p-20));
+      if (a.h_out) {  // int16 score image: its quantum, and ε widened to cover the codes
+        rr_quantum(eps * (1.0 + 0x1p-20), b, (double)a.istats[2], a.eps_out[row], a.h_out[row]);
+      } else {
+        a.eps_out[row] = __double2float_ru(eps * (1.0 + 0x1p-20));
+      }
     }
   }
 };
@@ -259,6 +263,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     if (a.out_f32) {
       for (int i = lane; i < a.Dpad_f; i += 64) a.out_f32[(size_t)row * a.Dpad_f + i] = 0.f;
       if (lane == 0) a.eps_out[row] = 0.f;
+      if (lane == 0 && a.h_out) a.h_out[row] = 0.f;
     }
     return;
   }

@@ -126,7 +126,10 @@ __device__ __forceinline__ void scan2_rr_prologue(const GemmArgs& a, int q, int 
     const double e = sqrt((double)e2 * sc), b = sqrt((double)b2 * sc);
     const double gam = 2.0 * (double)a.Kpad * 0x1p-24;
     const double eps = (double)a.q_istats[0] * b + (double)a.q_istats[1] * e + gam * (double)a.q_istats[2] * b;
-    a.q_eps_out[q] = __double2float_ru(eps * (1.0 + 0x1p-20));
+    if (a.q_h_out)
+      rr_quantum(eps * (1.0 + 0x1p-20), b, (double)a.q_istats[2], a.q_eps_out[q], a.q_h_out[q]);
+    else
+      a.q_eps_out[q] = __double2float_ru(eps * (1.0 + 0x1p-20));
   }
 }
 
@@ -389,8 +392,19 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
 
   const size_t w0 = (size_t)(a.slab_start >> 5);
   const uint32_t* erow = a.excl + (size_t)(q < a.M_valid ? q : a.M_valid - 1) * a.excl_ld;
-  float* Srow = a.S + (size_t)q * a.lds;
+  // score image: the blocked layout (sblk_quad) — store j of a tile writes the wave's 16
+  // accumulator quads j as one contiguous 1-KiB block (512 B as int16), eight full lines,
+  // where row-major S took 32 partial lines per store
+  const size_t sblk0 = (size_t)(q >> 5) * a.ldt * 1024 + lane * 4;  // + (tile·4 + j)·256
   constexpr bool STREAM = (ABL & kScanStream) != 0;
+  // int16 score image: this query's code scale 1/(h·32767) (h = 0: zero row, codes 0)
+  constexpr bool S16 = (ABL & kScanS16) != 0 && !STREAM;
+  float sk = 0.f;
+  if constexpr (S16) {
+    const float hq = q < a.M_valid ? a.s_h[q] : 0.f;
+    sk = hq > 0.f ? 1.0f / (hq * 32767.f) : 0.f;
+    asm volatile("" : "+v"(sk));  // consumed before any LDS-DMA is in flight
+  }
   StreamLane sl;
   const size_t region = ((size_t)q * n_chunks + chunk) * 2 + h;
   if constexpr (STREAM) stream_begin(a, q, region, sl);
@@ -479,7 +493,12 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
           } else if constexpr (s < 6) {
             if constexpr (epi && !(ABL & 8) && !STREAM) {
               constexpr int j = s - 2;
-              *(float4*)(Srow + ptile0 + 8 * j + 4 * h) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+              const size_t e = sblk0 + (size_t)(ptile * 4 + j) * 256;
+              if constexpr (S16)
+                *(uint2*)((int16_t*)a.S + e) =
+                    make_uint2(s16_pack(p[4 * j], p[4 * j + 1], sk), s16_pack(p[4 * j + 2], p[4 * j + 3], sk));
+              else
+                *(float4*)(a.S + e) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
             }
           } else if constexpr (s == 6) {
             if constexpr (epi && !(ABL & 16) && !STREAM) {
@@ -535,8 +554,14 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     te = te2 > te ? te2 : te;
     tp = tp2 > tp ? tp2 : tp;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      *(float4*)(Srow + tile * 32 + 8 * j + 4 * h) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+    for (int j = 0; j < 4; ++j) {
+      const size_t e = sblk0 + (size_t)(tile * 4 + j) * 256;
+      if constexpr (S16)
+        *(uint2*)((int16_t*)a.S + e) =
+            make_uint2(s16_pack(p[4 * j], p[4 * j + 1], sk), s16_pack(p[4 * j + 2], p[4 * j + 3], sk));
+      else
+        *(float4*)(a.S + e) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+    }
     (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
   };
 

@@ -29,6 +29,12 @@ static void launch_t(const GemmArgs& a, hipStream_t s) {
   const int tiles = a.Ncols / 32;
   const int n_chunks = scan4_n_chunks(a.Mpad, tiles);
   const int blocks = a.Mpad / kScan4Queries * n_chunks;
+  if constexpr (KU <= kRrMaxD / 8) {
+    if (a.s_h && !a.cand) {  // exact re-rank path: int16 score image
+      hipLaunchKernelGGL((scan4_kernel<KU, kScanS16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+      return;
+    }
+  }
   if (a.cand)
     hipLaunchKernelGGL((scan4_kernel<KU, kScanStream>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
   else

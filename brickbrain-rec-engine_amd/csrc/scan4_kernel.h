@@ -220,6 +220,14 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, i
   const uint32_t* erowA = a.excl + (size_t)(qA < a.M_valid ? qA : a.M_valid - 1) * a.excl_ld;
   const uint32_t* erowB = a.excl + (size_t)(qB < a.M_valid ? qB : a.M_valid - 1) * a.excl_ld;
   float* park = (float*)(smem + 2 * TILE_B) + wave * 1024;
+  // int16 score image (kScanS16): code scales 1/(h·32767) of the two query blocks
+  constexpr bool S16 = (ABL & kScanS16) != 0 && !STREAM;
+  float skA = 0.f, skB = 0.f;
+  if constexpr (S16) {
+    const float hA = qA < a.M_valid ? a.s_h[qA] : 0.f, hB = qB < a.M_valid ? a.s_h[qB] : 0.f;
+    skA = hA > 0.f ? 1.0f / (hA * 32767.f) : 0.f;
+    skB = hB > 0.f ? 1.0f / (hB * 32767.f) : 0.f;
+  }
   Stream4 slA, slB;
   auto region = [&](int q) __attribute__((always_inline)) { return ((size_t)q * n_chunks + chunk) * 2 + h; };
   if constexpr (STREAM) {  // bound = the last key of the query's pilot list (stream_begin)
@@ -247,6 +255,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, i
   // them would otherwise land behind later staging and wait for it
   asm volatile("" : "+v"(pw), "+v"(mw), "+v"(ewA), "+v"(ewB));
   if constexpr (STREAM) asm volatile("" : "+v"(slA.thr), "+v"(slB.thr), "+v"(slA.thrf), "+v"(slB.thrf));
+  if constexpr (S16) asm volatile("" : "+v"(skA), "+v"(skB));
   asm volatile("s_nop 4");
 
   f32x16s accA = {}, accB = {};
@@ -297,8 +306,14 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, i
       } else if constexpr (s <= 5) {
         if constexpr (!(ABL & 8)) {
           constexpr int j = s - 2;
-          float* dst = a.S + (((size_t)(q >> 5) * a.ldt + ptile) * 4 + j) * 256 + lane * 4;
-          *(float4*)dst = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+          const size_t e = (((size_t)(q >> 5) * a.ldt + ptile) * 4 + j) * 256 + lane * 4;
+          if constexpr (S16) {
+            const float sk = q == qA ? skA : skB;
+            *(uint2*)((int16_t*)a.S + e) =
+                make_uint2(s16_pack(p[4 * j], p[4 * j + 1], sk), s16_pack(p[4 * j + 2], p[4 * j + 3], sk));
+          } else {
+            *(float4*)(a.S + e) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
+          }
         }
       } else if constexpr (s == 6) {
         if constexpr (!(ABL & 16)) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;

@@ -37,6 +37,24 @@ constexpr int kR0Cap = 32;
 constexpr int kOffQs = kOffR0 + kR0Cap * 4;       // fused re-rank: the f32 query row
 constexpr int kSelectLds = kOffQs + kRrMaxD * 4;
 
+// Scores of the slab: element index of item quad g of tile t of a row (row-major S, or the
+// blocked image), and the loads — f32, or int16 codes times the row's quantum (s_h).
+__device__ __forceinline__ size_t s_elem(const SelectArgs& a, int row, int t, int g) {
+  return a.s_blocked ? sblk_quad(row, t, g, a.ldt) : (size_t)row * a.lds + t * 32 + 4 * g;
+}
+__device__ __forceinline__ float4 s_quad_ld(const SelectArgs& a, int row, int t, int g, float sh) {
+  const size_t e = s_elem(a, row, t, g);
+  if (a.s_h) {
+    const uint2 w = *(const uint2*)((const int16_t*)a.S + e);
+    return make_float4(s16_lo(w.x, sh), s16_hi(w.x, sh), s16_lo(w.y, sh), s16_hi(w.y, sh));
+  }
+  return *(const float4*)(a.S + e);
+}
+__device__ __forceinline__ float s_at_ld(const SelectArgs& a, int row, int j, float sh) {
+  const size_t e = s_elem(a, row, j >> 5, (j >> 2) & 7) + (j & 3);
+  return a.s_h ? (float)((const int16_t*)a.S)[e] * sh : a.S[e];
+}
+
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t x = v;
@@ -452,14 +470,10 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   if (RR && a.rr_flags && a.rr_flags[row] == 0u) return;  // finished by select_rr_wave_kernel
   const int n = a.n_cols, K = a.K;
   const int ntiles = (n + 31) >> 5;
-  const float* Srow = a.S + (size_t)row * a.lds;
   // four scores of items 4g..4g+3 of tile t (row-major S or the scan3 blocked image)
-  auto s_quad = [&](int t, int g) -> float4 {
-    return a.s_blocked ? *(const float4*)(a.S + sblk_quad(row, t, g, a.ldt)) : *(const float4*)(Srow + t * 32 + 4 * g);
-  };
-  auto s_at = [&](int j) -> float {
-    return a.s_blocked ? a.S[sblk_quad(row, j >> 5, (j >> 2) & 7, a.ldt) + (j & 3)] : Srow[j];
-  };
+  const float sh = a.s_h ? a.s_h[row] : 0.f;  // int16 score image: decode quantum
+  auto s_quad = [&](int t, int g) -> float4 { return s_quad_ld(a, row, t, g, sh); };
+  auto s_at = [&](int j) -> float { return s_at_ld(a, row, j, sh); };
   const uint32_t* trow = a.tmax + (size_t)row * a.ldt;
   const uint32_t* prow = a.max_inout ? a.pmax + (size_t)row * a.ldt : nullptr;
   const uint32_t* excl = a.excl ? a.excl + (size_t)row * a.excl_ld : nullptr;
@@ -1178,10 +1192,8 @@ __global__ __launch_bounds__(kSelectThreads) void rerank_kernel(SelectArgs a) {
   uint32_t* misc = (uint32_t*)(dsm + kRrOffMisc);
   const int row = xcd_row(blockIdx.x, gridDim.x), tid = threadIdx.x;
   const int n = a.n_cols;
-  const float* Srow = a.S + (size_t)row * a.lds;
-  auto s_at = [&](int j) -> float {
-    return a.s_blocked ? a.S[sblk_quad(row, j >> 5, (j >> 2) & 7, a.ldt) + (j & 3)] : Srow[j];
-  };
+  const float sh = a.s_h ? a.s_h[row] : 0.f;
+  auto s_at = [&](int j) -> float { return s_at_ld(a, row, j, sh); };
   const uint32_t* excl = a.excl ? a.excl + (size_t)row * a.excl_ld : nullptr;
   const int64_t w0 = a.slab_start >> 5;
   auto elig = [&](int tile) -> uint32_t {
@@ -1258,13 +1270,9 @@ __global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
   const int row = xcd_row(blockIdx.x, gridDim.x), lane = threadIdx.x;
   const int n = a.n_cols, K = a.K;
   const int ntiles = (n + 31) >> 5;
-  const float* Srow = a.S + (size_t)row * a.lds;
-  auto s_quad = [&](int t, int g) -> float4 {
-    return a.s_blocked ? *(const float4*)(a.S + sblk_quad(row, t, g, a.ldt)) : *(const float4*)(Srow + t * 32 + 4 * g);
-  };
-  auto s_at = [&](int j) -> float {
-    return a.s_blocked ? a.S[sblk_quad(row, j >> 5, (j >> 2) & 7, a.ldt) + (j & 3)] : Srow[j];
-  };
+  const float sh = a.s_h ? a.s_h[row] : 0.f;  // int16 score image: decode quantum
+  auto s_quad = [&](int t, int g) -> float4 { return s_quad_ld(a, row, t, g, sh); };
+  auto s_at = [&](int j) -> float { return s_at_ld(a, row, j, sh); };
   const uint32_t* trow = a.tmax + (size_t)row * a.ldt;
   const uint32_t* prow = a.max_inout ? a.pmax + (size_t)row * a.ldt : nullptr;
   const uint32_t* excl = a.excl ? a.excl + (size_t)row * a.excl_ld : nullptr;
