@@ -143,12 +143,20 @@ __host__ __device__ inline size_t t3_chunk_offset(int64_t row, int c, int P, int
   return (size_t)(row >> 5) * 32 * 3 * Dpad * 2 + ((size_t)(P * KP + c) * 32 + (row & 31)) * 16;
 }
 
-// scan3 score image ("blocked S"): each (32-query block, tile) accumulator stored as the MFMA
-// leaves it, 4 KiB contiguous, so the scan's score stores are full 1-KiB wave writes.  Items
-// 4g..4g+3 (g = item >> 2 within the tile) of query q are the float4 at the returned float
-// offset; ldt = tiles per query row.
+// Score image of the scan kernels ("blocked S"): each (32-query block, tile) accumulator
+// stored as 4 KiB contiguous, so every score store is a full 1-KiB wave write (512 B as
+// int16).  Store j (accumulator quads j of both lane halves) fills one 1-KiB block; lane
+// (r, h) = (query q & 31, half) writes its quad at position 2r + h, so the two halves of a
+// query sit side by side: a query's tile spans 4 lines of 4 queries each (32 B per query per
+// line), where lane order h·32 + r spread it over 8.  Items 4g..4g+3 (g = item >> 2 within
+// the tile; j = g >> 1, h = g & 1) of query q are the float4 at the returned element offset;
+// ldt = tiles per query row.
 __host__ __device__ inline size_t sblk_quad(int q, int t, int g, int64_t ldt) {
-  return (((size_t)(q >> 5) * ldt + t) * 4 + (g >> 1)) * 256 + (((g & 1) << 5) | (q & 31)) * 4;
+  return (((size_t)(q >> 5) * ldt + t) * 4 + (g >> 1)) * 256 + (2 * (q & 31) + (g & 1)) * 4;
+}
+// element offset of lane (r, h)'s quads inside its wave's block: + (tile·4 + j)·256
+__host__ __device__ inline size_t sblk_lane(int q, int h, int64_t ldt) {
+  return (size_t)(q >> 5) * ldt * 1024 + (2 * (q & 31) + h) * 4;
 }
 
 // XCD-aware bijection blockIdx -> row of [0, total): workgroup L runs on XCD L & 7, and each

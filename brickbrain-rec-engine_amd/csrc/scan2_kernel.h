@@ -395,7 +395,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   // score image: the blocked layout (sblk_quad) — store j of a tile writes the wave's 16
   // accumulator quads j as one contiguous 1-KiB block (512 B as int16), eight full lines,
   // where row-major S took 32 partial lines per store
-  const size_t sblk0 = (size_t)(q >> 5) * a.ldt * 1024 + lane * 4;  // + (tile·4 + j)·256
+  const size_t sblk0 = sblk_lane(q, h, a.ldt);  // + (tile·4 + j)·256
   constexpr bool STREAM = (ABL & kScanStream) != 0;
   // int16 score image: this query's code scale 1/(h·32767) (h = 0: zero row, codes 0)
   constexpr bool S16 = (ABL & kScanS16) != 0 && !STREAM;

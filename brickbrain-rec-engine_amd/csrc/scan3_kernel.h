@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
   const size_t w0 = (size_t)(a.slab_start >> 5);
   const uint32_t* erow = a.excl + (size_t)(q < a.M_valid ? q : a.M_valid - 1) * a.excl_ld;
   // blocked score image (sblk_quad): this wave's 4-KiB block per tile, lane-linear
-  float* Sblk = a.S + (size_t)(q >> 5) * a.ldt * 1024 + lane * 4;
+  float* Sblk = a.S + sblk_lane(q, h, a.ldt);
   constexpr bool STREAM = (ABL & kScanStream) != 0;
   StreamLane sl;
   const size_t region = ((size_t)q * n_chunks + chunk) * 2 + h;

@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, i
       } else if constexpr (s <= 5) {
         if constexpr (!(ABL & 8)) {
           constexpr int j = s - 2;
-          const size_t e = (((size_t)(q >> 5) * a.ldt + ptile) * 4 + j) * 256 + lane * 4;
+          const size_t e = sblk_lane(q, h, a.ldt) + (size_t)(ptile * 4 + j) * 256;
           if constexpr (S16) {
             const float sk = q == qA ? skA : skB;
             *(uint2*)((int16_t*)a.S + e) =
