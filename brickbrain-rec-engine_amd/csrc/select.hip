@@ -1378,8 +1378,11 @@ __global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
   // ---- gather: eight lanes per qualifying tile (one 16-B score quad each, so a wave load
   // reads eight whole 128-B tile rows), up to 128 tiles per round with every load issued
   // before any is used ----
+  // candidates are compacted by ballots (a uniform running count, no LDS atomics: the
+  // lanes of a round hitting one counter serialised the atomics)
+  uint32_t nc = 0;
   {
-    constexpr int kGP = 16;  // tiles per lane group per round
+    constexpr int kGP = 24;  // tiles per lane group per round: one round up to 192 tiles
     const int sub = lane & 7, grp = lane >> 3;
     for (uint32_t base = 0; base < ntl; base += 8 * kGP) {
       float4 v[kGP];
@@ -1406,18 +1409,19 @@ __global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
           const int it = 4 * sub + c;
           m |= (t >= 0 && t * 32 + it < n && ((okw[p] >> it) & 1u) && ord_of(f[c]) >= Tg) ? (1u << c) : 0u;
         }
-        if (m) {
-          uint32_t q = atomicAdd(&misc[0], (uint32_t)__popc(m));
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if ((m >> c) & 1u) {
-              if (q < (uint32_t)kWvCand) cand[q] = make_key(ord_of(f[c]), a.gid0 + (uint32_t)(t * 32 + 4 * sub + c));
-              ++q;
-            }
+        for (int c = 0; c < 4; ++c) {
+          const uint64_t bm = __ballot((m >> c) & 1u);
+          if ((m >> c) & 1u) {
+            const uint32_t q = nc + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+            if (q < (uint32_t)kWvCand) cand[q] = make_key(ord_of(f[c]), a.gid0 + (uint32_t)(t * 32 + 4 * sub + c));
+          }
+          nc += (uint32_t)__popcll(bm);
         }
       }
     }
   }
+  if (lane == 0) misc[0] = nc;
   // rank-0 items: present, within the margin of the present maximum
   uint64_t* r0k = cand + kWvCand;
   for (uint32_t i = lane; i < nt0 * 32; i += 64) {
