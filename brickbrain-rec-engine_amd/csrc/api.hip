@@ -742,8 +742,11 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     const bool s16_on = s16_env == 1 || (s16_env == 2 && scan4_used(BF16, bpad));
     const bool s16_c = s16_on && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
     const bool s16_f = s16_on && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
-    if (need_content && !fuse_c && !rrfuse_c) {
-      PrepArgs pa{};
+    // the prep launches of both sides (hybrid) go out as one launch
+    const bool prep_c = need_content && !fuse_c && !rrfuse_c, prep_f = need_cf && !fuse_f && !rrfuse_f;
+    PrepArgs pa_c{}, pa_f{};
+    if (prep_c) {
+      PrepArgs& pa = pa_c;
       pa.Bpad = bpad;
       pa.B = bc;
       pa.d = x->d;
@@ -770,10 +773,9 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         pa.src_ld = x->d;
         pa.normalize = q->mode == BB_MODE_SEMANTIC ? 1 : 0;
       }
-      if ((rc = timed(x, K_PREP, s, [&] { return launch_prep(pa, s); }))) return rc;
     }
-    if (need_cf && !fuse_f && !rrfuse_f) {
-      PrepArgs pa{};
+    if (prep_f) {
+      PrepArgs& pa = pa_f;
       pa.Bpad = bpad;
       pa.B = bc;
       pa.d = x->r;
@@ -793,7 +795,11 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       pa.src_dtype = q->q_cf_dtype;
       pa.src_ld = x->r;
       pa.normalize = 0;
-      if ((rc = timed(x, K_PREP, s, [&] { return launch_prep(pa, s); }))) return rc;
+    }
+    if (prep_c && prep_f) {
+      if ((rc = timed(x, K_PREP, s, [&] { return launch_prep2(pa_c, pa_f, s); }))) return rc;
+    } else if (prep_c || prep_f) {
+      if ((rc = timed(x, K_PREP, s, [&] { return launch_prep(prep_c ? pa_c : pa_f, s); }))) return rc;
     }
     // ---- per side: slabs of gemm + select ----
     int final_pp = 0;

@@ -313,6 +313,7 @@ hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s);
 hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s);
+hipError_t launch_prep2(const PrepArgs& a0, const PrepArgs& a1, hipStream_t s);
 hipError_t launch_mask(const MaskArgs& a, hipStream_t s);
 hipError_t launch_clear_bits(uint32_t* bits, const int64_t* ids, int64_t n_ids, int64_t n_items,
                              hipStream_t s);

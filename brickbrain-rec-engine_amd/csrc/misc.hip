@@ -241,8 +241,8 @@ struct RrAcc {
   }
 };
 
-__global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void prep_rows(const PrepArgs& a, int blk) {
+  const int row = blk * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= a.Bpad) return;
   const void* src = a.src;
@@ -321,9 +321,26 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   if (a.out_f32) rr.finish(a, row, lane);
 }
 
+__global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) { prep_rows(a, blockIdx.x); }
+
+// both sides of a hybrid search in one launch: blocks [0, nb0) prep a0, the rest a1
+__global__ __launch_bounds__(256) void prep2_kernel(PrepArgs a0, PrepArgs a1, int nb0) {
+  if ((int)blockIdx.x < nb0)
+    prep_rows(a0, blockIdx.x);
+  else
+    prep_rows(a1, blockIdx.x - nb0);
+}
+
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s) {
   if (a.Bpad <= 0) return hipSuccess;
   hipLaunchKernelGGL(prep_kernel, dim3((a.Bpad + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep2(const PrepArgs& a0, const PrepArgs& a1, hipStream_t s) {
+  if (a0.Bpad <= 0 || a1.Bpad <= 0) return hipErrorInvalidValue;
+  const int nb0 = (a0.Bpad + 3) / 4, nb1 = (a1.Bpad + 3) / 4;
+  hipLaunchKernelGGL(prep2_kernel, dim3(nb0 + nb1), dim3(256), 0, s, a0, a1, nb0);
   return hipGetLastError();
 }
 
@@ -419,24 +436,50 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
     if (a.counts && tid == 0) a.counts[q] = n;
     return;
   }
-  // union blend (recommendation_system.py:789-843): content entries, then CF-only entries
+  // union blend (recommendation_system.py:789-843): content entries, then CF-only entries.
+  // CF ids go into an LDS hash table (open addressing, 2·kMaxKInt slots: load <= 1/2); each
+  // content entry looks its id up there and marks the CF entry it consumed.
   const uint64_t* L0 = lst[0] + start[0];
   const uint64_t* L1 = lst[1] + start[1];
+  constexpr int kTab = 2 * kMaxKInt;
+  __shared__ uint32_t tab_g[kTab];   // gid + 1 (0 = empty)
+  __shared__ uint16_t tab_j[kTab];
+  __shared__ uint8_t used[kMaxKInt];
+  for (int i = tid; i < kTab; i += kFinThreads) tab_g[i] = 0u;
+  for (int j = tid; j < c[1]; j += kFinThreads) used[j] = 0;
+  __syncthreads();
+  auto slot0 = [](uint32_t g) { return (int)((g * 2654435761u) >> 22) & (kTab - 1); };
+  for (int j = tid; j < c[1]; j += kFinThreads) {
+    const uint32_t g = gid_of(L1[j]);
+    for (int sl = slot0(g);; sl = (sl + 1) & (kTab - 1))
+      if (atomicCAS(&tab_g[sl], 0u, g + 1u) == 0u) {
+        tab_j[sl] = (uint16_t)j;
+        break;
+      }
+  }
+  __syncthreads();
   for (int i = tid; i < c[0]; i += kFinThreads) {
     const uint32_t g = gid_of(L0[i]);
     int hit = -1;
-    for (int j = 0; j < c[1]; ++j) hit = gid_of(L1[j]) == g ? j : hit;
+    for (int sl = slot0(g);; sl = (sl + 1) & (kTab - 1)) {
+      const uint32_t t = tab_g[sl];
+      if (t == 0u) break;
+      if (t == g + 1u) {
+        hit = tab_j[sl];
+        break;
+      }
+    }
+    if (hit >= 0) used[hit] = 1;
     const double cs = (double)float_of_ord(ordk_of(L0[i]));
     const double fs = hit >= 0 ? (double)float_of_ord(ordk_of(L1[hit])) : 0.0;
     eh[i] = a.w_content * cs + a.w_cf * fs;
     ek[i] = ord64_of(eh[i]);
     eg[i] = g;
   }
+  __syncthreads();
   for (int j = tid; j < c[1]; j += kFinThreads) {
     const uint32_t g = gid_of(L1[j]);
-    bool in_c = false;
-    for (int i = 0; i < c[0]; ++i) in_c |= gid_of(L0[i]) == g;
-    if (!in_c) {
+    if (!used[j]) {
       const int pos = c[0] + atomicAdd(&n_ent, 1);
       eh[pos] = a.w_content * 0.0 + a.w_cf * (double)float_of_ord(ordk_of(L1[j]));
       ek[pos] = ord64_of(eh[pos]);
@@ -450,6 +493,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
     const uint64_t hk = ek[e];
     const uint32_t g = eg[e];
     int rank = 0;
+#pragma unroll 8
     for (int f = 0; f < ne; ++f) rank += (ek[f] > hk) || (ek[f] == hk && eg[f] < g);
     if (rank < a.k) {
       sc[rank] = (float)eh[e];
