@@ -606,7 +606,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   // workspace
   const size_t es = elem_size(x->dtype);
   if ((rc = x->S.ensure((size_t)Bc * lds * 4))) return rc;
-  if ((rc = x->tmax.ensure((size_t)Bc * ldt * 4 * 2))) return rc;  // tmax + pmax
+  // tmax + pmax, twice for the dual hybrid launch (both sides' scans before both selects)
+  if ((rc = x->tmax.ensure((size_t)Bc * ldt * 4 * 2 * (q->mode == BB_MODE_HYBRID ? 2 : 1)))) return rc;
   // query rows: index dtype, or three bf16 planes (6 B / element) for the split scan
   const size_t qes_c = x->items3.p ? std::max<size_t>(es, 6) : es, qes_f = x->cf3.p ? std::max<size_t>(es, 6) : es;
   if (need_content && (rc = x->qn.ensure(std::max((size_t)Bc * x->Dpad * qes_c, (size_t)Bc * x->Dpad_b * 2)))) return rc;
@@ -802,6 +803,20 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       if ((rc = timed(x, K_PREP, s, [&] { return launch_prep(prep_c ? pa_c : pa_f, s); }))) return rc;
     }
     // ---- per side: slabs of gemm + select ----
+    // Hybrid on the exact re-rank path with both sides on scan4 + the one-wave select: the two
+    // sides' scans go out as ONE launch and their selects as one (scan4_dual_kernel,
+    // select_rr_wave_dual_kernel); each side keeps its own half of the int16 image and its own
+    // maxima / flag rows.  Measured (r02za, configs[2]): serial p50 222 -> 173 us (scan 86 ->
+    // 77 us, select 116 -> 62 us per step); with three batches in flight 6.6 -> 6.3 M q/s.
+    // BB_DUAL=0 (A/B runs) keeps one launch per side.
+    static const bool dual_env = !(getenv("BB_DUAL") && atoi(getenv("BB_DUAL")) == 0);
+    static const int sel_wave_env0 = getenv("BB_SELECT_WAVE") ? atoi(getenv("BB_SELECT_WAVE")) : -1;
+    const bool dual = dual_env && q->mode == BB_MODE_HYBRID && sides == 2 && s16_c && s16_f && !stream &&
+                      n_slabs == 1 && scan4_used(BF16, bpad) && scan4_dual_supported((int)x->Dpad_b / 8, (int)x->Rpad_b / 8) &&
+                      std::min<int64_t>(slab, x->n) <= 32768 && K_int <= 256 && sel_wave_env0 != 0 && bc > 256;
+    if (dual && (rc = x->rr_flags.ensure((size_t)Bc * 4 * 2))) return rc;
+    GemmArgs ga_dual0{};
+    SelectArgs sa_dual0{};
     int final_pp = 0;
     for (int side = 0; side < sides; ++side) {
       const bool cf_side = (q->mode == BB_MODE_CF) || (q->mode == BB_MODE_HYBRID && side == 1);
@@ -836,8 +851,9 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         ga.present = (const uint32_t*)(cf_side ? x->cf_present.p : x->items_present.p);
         ga.excl = has_excl ? (const uint32_t*)d_excl + (size_t)b0 * nw : (const uint32_t*)x->zeros.p;
         ga.excl_ld = has_excl ? nw : 0;
-        ga.tmax = (uint32_t*)x->tmax.p;
-        ga.pmax = (uint32_t*)x->tmax.p + (size_t)Bc * ldt;
+        ga.tmax = (uint32_t*)x->tmax.p + (dual && side ? (size_t)Bc * ldt * 2 : 0);
+        ga.pmax = ga.tmax + (size_t)Bc * ldt;
+        if (dual && side) ga.S = (float*)((int16_t*)x->S.p + (size_t)Bc * lds);  // the image's second half
         ga.ldt = ldt;
         int regions = 0, cand_cap = 0;
         if (spass) {
@@ -893,7 +909,13 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           ga.ldx = ga.ldq = w;
           ga.Kpad = (int)w;
           ga.s_h = (cf_side ? s16_f : s16_c) ? (const float*)(cf_side ? x->qcfh.p : x->qh.p) : nullptr;
-          if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(BF16, ga, s); }))) return rc;
+          if (dual && side == 0) {
+            ga_dual0 = ga;  // launched with side 1's
+          } else if (dual) {
+            if ((rc = timed(x, K_GEMM, s, [&] { return launch_scan4_dual(ga_dual0, ga, s); }))) return rc;
+          } else if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(BF16, ga, s); }))) {
+            return rc;
+          }
         } else if (cf_side ? s3_f : s3_c) {
           // split-precision scan: items, gathered rows and prepped queries are bf16 planes
           const int64_t w = ga.ldq;
@@ -1001,6 +1023,17 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           sa.rr_thr = (uint32_t*)x->rr_thr.p;
           sa.rr_r0 = (uint32_t*)x->rr_r0.p;
           sa.rr_r0n = (uint32_t*)x->rr_r0n.p;
+        }
+        if (dual) {
+          sa.S = ga.S;
+          sa.rr_flags = (uint32_t*)x->rr_flags.p + (side ? Bc : 0);
+          if (side == 0) {
+            sa_dual0 = sa;  // launched with side 1's
+          } else if ((rc = timed(x, K_SELECT, s, [&] { return launch_select_rr_wave_dual(sa_dual0, sa, bc, s); }))) {
+            return rc;
+          }
+          final_pp = pp;
+          continue;
         }
         if (sel_wave) {
           if ((rc = x->rr_flags.ensure((size_t)Bc * 4))) return rc;

@@ -297,6 +297,8 @@ bool scan4_used(int dtype, int Mpad);                // bf16 scan with 64 querie
 // item chunks (candidate regions / 2 per query) of the scan launch for these shapes
 int scan_chunks(int dtype, int Mpad, int tiles, bool split);
 bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s);  // scan4_used(BF16, a.Mpad) shapes
+bool scan4_dual_supported(int ku0, int ku1);
+hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s);  // hybrid, int16 image
 hipError_t launch_scan3(const GemmArgs& a, hipStream_t s);  // X = item planes, Q = q3f image
 hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t* dst, hipStream_t s);
 // f32 rows [Npad][ld_f] -> bf16 copy [Npad][ld_b] (RNE, zero padded) + error statistics
@@ -310,6 +312,7 @@ hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s);
 hipError_t launch_rerank(const SelectArgs& a, int B, hipStream_t s);  // after launch_select, rr_* set
 // one wave per query, one-slab re-rank searches (rr_flags set; rows it leaves: launch_select)
 hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s);
+hipError_t launch_select_rr_wave_dual(const SelectArgs& a0, const SelectArgs& a1, int B, hipStream_t s);
 hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s);

@@ -41,6 +41,43 @@ static void launch_t(const GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((scan4_kernel<KU>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
 }
 
+// The hybrid's two re-rank scans (int16 image) in one launch: content rows of 192..512
+// (KU0 in {24, 32, 48, 64}), CF factors up to 128 wide (KU1 in {8, 16}).
+template <int KU0, int KU1>
+static void launch_dual_t(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  const int t0 = a0.Ncols / 32, t1 = a1.Ncols / 32;
+  const int nc0 = scan4_n_chunks(a0.Mpad, t0), nc1 = scan4_n_chunks(a1.Mpad, t1);
+  const int nb0 = a0.Mpad / kScan4Queries * nc0, nb1 = a1.Mpad / kScan4Queries * nc1;
+  hipLaunchKernelGGL((scan4_dual_kernel<KU0, KU1, kScanS16>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0, s, a0, a1,
+                     nc0, t0, nc1, t1, nb0);
+}
+template <int KU0>
+static bool launch_dual_k1(const GemmArgs& a0, const GemmArgs& a1, int ku1, hipStream_t s) {
+  switch (ku1) {
+    case 8: launch_dual_t<KU0, 8>(a0, a1, s); return true;
+    case 16: launch_dual_t<KU0, 16>(a0, a1, s); return true;
+    default: return false;
+  }
+}
+bool scan4_dual_supported(int ku0, int ku1) {
+  return (ku0 == 24 || ku0 == 32 || ku0 == 48 || ku0 == 64) && (ku1 == 8 || ku1 == 16);
+}
+hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  const int ku0 = a0.Kpad * 2 / 16, ku1 = a1.Kpad * 2 / 16;
+  if (!scan4_dual_supported(ku0, ku1) || !a0.s_h || !a1.s_h || a0.cand || a1.cand || !scan4_used(BF16, a0.Mpad) ||
+      a0.Mpad != a1.Mpad || a0.Ncols % 32 || a1.Ncols % 32 || (a0.slab_start & 31) || (a1.slab_start & 31) || a0.q_ids ||
+      a0.q_src || a0.q_istats || a1.q_ids || a1.q_src || a1.q_istats)
+    return hipErrorInvalidValue;
+  bool ok = false;
+  switch (ku0) {
+    case 24: ok = launch_dual_k1<24>(a0, a1, ku1, s); break;
+    case 32: ok = launch_dual_k1<32>(a0, a1, ku1, s); break;
+    case 48: ok = launch_dual_k1<48>(a0, a1, ku1, s); break;
+    case 64: ok = launch_dual_k1<64>(a0, a1, ku1, s); break;
+  }
+  return ok ? hipGetLastError() : hipErrorInvalidValue;
+}
+
 bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s) {
   switch (ku) {
     case 8: launch_t<8>(a, s); return true;

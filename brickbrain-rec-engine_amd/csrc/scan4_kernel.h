@@ -129,7 +129,7 @@ constexpr int scan4_atA(int s, int U, int E, int pieces) {
 // per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no streaming
 // appends (compares only), 64 = streaming appends without their stores.
 template <int KU, int ABL = 0>
-__global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, int n_chunks, int tiles_total) {
+__device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int tiles_total, int L) {
   typedef uint16_t T;
   constexpr int U = KU / 2;        // u-steps (one bf16 MFMA each) per tile and block
   constexpr int ROWB = KU * 16;
@@ -148,7 +148,6 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, i
 
   const int n_groups = a.Mpad / kScan4Queries;
   const int total = n_groups * n_chunks;
-  const int L = blockIdx.x;
   const int xcd = L & 7, local = L >> 3, q8 = total >> 3, r8 = total & 7;
   const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
   const int chunk = t / n_groups, group = t - chunk * n_groups;
@@ -563,6 +562,23 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, i
     }
   }
   }  // !IL
+}
+
+template <int KU, int ABL = 0>
+__global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_kernel(GemmArgs a, int n_chunks, int tiles_total) {
+  scan4_body<KU, ABL>(a, n_chunks, tiles_total, blockIdx.x);
+}
+
+// Both sides of a hybrid search in one launch (content KU0, CF KU1): workgroups [0, nb0)
+// scan side 0, the rest side 1 — one launch ramp and tail, and the CF side's short tiles
+// fill the CUs beside the content side's long ones.
+template <int KU0, int KU1, int ABL>
+__global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_dual_kernel(GemmArgs a0, GemmArgs a1, int nc0, int t0,
+                                                                        int nc1, int t1, int nb0) {
+  if ((int)blockIdx.x < nb0)
+    scan4_body<KU0, ABL>(a0, nc0, t0, blockIdx.x);
+  else
+    scan4_body<KU1, ABL>(a1, nc1, t1, blockIdx.x - nb0);
 }
 
 }  // namespace bb

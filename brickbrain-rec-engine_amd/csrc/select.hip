@@ -456,7 +456,7 @@ __device__ const uint32_t kWordZero = 0u;
 // RR: the re-rank variant (rr_eps set) — a separate instance, so the plain select keeps its
 // register budget
 template <int ABL, bool RR = false>
-__global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
+__device__ __forceinline__ void select_body(const SelectArgs& a, int row) {
   __shared__ __attribute__((aligned(16))) char dsm[kSelectLds];
   uint64_t* cand = (uint64_t*)dsm;
   uint32_t* hist = (uint32_t*)(dsm + kOffHist);
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   uint32_t* scan_sh = misc + 16;                  // 8 words
   uint64_t* red = (uint64_t*)(misc + 32);         // 4 u64
 
-  const int row = xcd_row(blockIdx.x, gridDim.x), tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (RR && a.rr_flags && a.rr_flags[row] == 0u) return;  // finished by select_rr_wave_kernel
   const int n = a.n_cols, K = a.K;
   const int ntiles = (n + 31) >> 5;
@@ -910,6 +910,18 @@ __global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
   for (int i = tid; i < K; i += kSelectThreads) out[i] = i < (int)cnt ? cand[i] : 0ull;
 }
 
+template <int ABL, bool RR = false>
+__global__ __launch_bounds__(kSelectThreads) void select_kernel(SelectArgs a) {
+  select_body<ABL, RR>(a, xcd_row(blockIdx.x, gridDim.x));
+}
+// re-rank rows the hybrid's dual wave select left (rr_flags), both sides in one launch
+__global__ __launch_bounds__(kSelectThreads) void select_rr_dual_kernel(SelectArgs a0, SelectArgs a1, int B0, int B1) {
+  if ((int)blockIdx.x < B0)
+    select_body<0, true>(a0, xcd_row(blockIdx.x, B0));
+  else
+    select_body<0, true>(a1, xcd_row(blockIdx.x - B0, B1));
+}
+
 // ---- streaming top-K, second stage -------------------------------------------------------
 // The K-th largest of n distinct keys (get(i), non-zero) by a 64-bit radix select in six
 // digit passes (12/12/12/12/8/8 bits); 0 when n < K (take every key).
@@ -1260,14 +1272,14 @@ __device__ __forceinline__ void wave_rescore_any(uint64_t* keys, int m, const Se
 }
 
 template <int UM>
-__global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
+__device__ __forceinline__ void select_rr_wave_body(const SelectArgs& a, int row) {
   __shared__ __attribute__((aligned(16))) char dsm[kWvLds];
   uint64_t* cand = (uint64_t*)(dsm + kWvOffCand);
   uint32_t* tl = (uint32_t*)(dsm + kWvOffTl);
   uint32_t* r0t = (uint32_t*)(dsm + kWvOffR0t);
   float* qs = (float*)(dsm + kWvOffQs);
   uint32_t* misc = (uint32_t*)(dsm + kWvOffMisc);
-  const int row = xcd_row(blockIdx.x, gridDim.x), lane = threadIdx.x;
+  const int lane = threadIdx.x;
   const int n = a.n_cols, K = a.K;
   const int ntiles = (n + 31) >> 5;
   const float sh = a.s_h ? a.s_h[row] : 0.f;  // int16 score image: decode quantum
@@ -1460,6 +1472,18 @@ __global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
   if (a.trace && lane == 0) a.trace[row * 8 + 6] = cnt, a.trace[row * 8 + 7] = ntl;
 }
 
+template <int UM>
+__global__ __launch_bounds__(64) void select_rr_wave_kernel(SelectArgs a) {
+  select_rr_wave_body<UM>(a, xcd_row(blockIdx.x, gridDim.x));
+}
+// both sides of a hybrid search: workgroups [0, B0) side 0, the rest side 1
+__global__ __launch_bounds__(64) void select_rr_wave_dual_kernel(SelectArgs a0, SelectArgs a1, int B0, int B1) {
+  if ((int)blockIdx.x < B0)
+    select_rr_wave_body<2>(a0, xcd_row(blockIdx.x, B0));
+  else
+    select_rr_wave_body<2>(a1, xcd_row(blockIdx.x - B0, B1));
+}
+
 hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s) {
   if (!a.rr_eps || !a.rr_x || !a.rr_q || !a.rr_flags || a.rr_out || a.carry_in || a.rr_d <= 0 || a.rr_d > kRrMaxD ||
       (a.rr_d & 3) || a.K <= 0 || a.K > kWvCand || B <= 0 || a.n_cols <= 0 || a.n_cols > 64 * kWvTPL * 32 || !a.tmax ||
@@ -1472,6 +1496,20 @@ hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s) {
     hipLaunchKernelGGL(select_rr_wave_kernel<2>, dim3(B), dim3(64), 0, s, a);
   else
     hipLaunchKernelGGL(select_rr_wave_kernel<1>, dim3(B), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+// Both sides of a hybrid re-rank search (one slab, query chunks > 256 rows): the one-wave
+// selects of the two sides in one launch, then the block select of the rows they left.
+hipError_t launch_select_rr_wave_dual(const SelectArgs& a0, const SelectArgs& a1, int B, hipStream_t s) {
+  for (const SelectArgs* a : {&a0, &a1})
+    if (!a->rr_eps || !a->rr_x || !a->rr_q || !a->rr_flags || a->rr_out || a->carry_in || a->rr_d <= 0 ||
+        a->rr_d > kRrMaxD || (a->rr_d & 3) || a->K <= 0 || a->K > kWvCand || B <= 0 || a->n_cols <= 0 ||
+        a->n_cols > 64 * kWvTPL * 32 || !a->tmax || (a->max_inout && !a->pmax) || (a->slab_start & 31) ||
+        a->out_scores || a->rr_d > 4 * kSelectThreads)
+      return hipErrorInvalidValue;
+  hipLaunchKernelGGL(select_rr_wave_dual_kernel, dim3(2 * B), dim3(64), 0, s, a0, a1, B, B);
+  hipLaunchKernelGGL(select_rr_dual_kernel, dim3(2 * B), dim3(kSelectThreads), 0, s, a0, a1, B, B);
   return hipGetLastError();
 }
 
