@@ -65,8 +65,9 @@ def scan_kernel_info(dtype, width, batch):
     if dtype == "f32" and os.environ.get("BB_NO_RR"):
         return "scan2_kernel<float> (fp32 MFMA)", 1.0
     if dtype == "f32":
-        return (f"{kern}<uint16_t,{width * 2 // 16}> (one-product bf16 approximate scan; "
-                f"exact f32 re-rank of the candidates in rerank_kernel)"), 1.0
+        sel = "rerank_kernel" if batch <= 256 else "the one-wave select"
+        return (f"{kern}<uint16_t,{width * 2 // 16}> (one-product bf16 approximate scan, int16 score image; "
+                f"exact f32 re-rank of the candidates in {sel})"), 1.0
     return f"{kern}<uint16_t,{width * 2 // 16}> (bf16 MFMA)", 1.0
 
 
@@ -469,6 +470,9 @@ def main():
         flops = 2.0 * B * N_ITEMS * (DIM + r)
         alg_bytes = N_ITEMS * (DIM + r) * es + B * (r * 4 + 8) + B * TOPK * 12 + N_ITEMS // 8
         kname, mpf = scan_kernel_info(args.dtype, DIM, B)
+        if args.dtype == "f32" and not os.environ.get("BB_NO_RR") and os.environ.get("BB_DUAL", "1") != "0":
+            kname = ("scan4_dual_kernel<48,8> (content d=384 + CF r=50 one-product bf16 scans in one launch, "
+                     "int16 score image; exact f32 re-rank of the candidates in the one-wave select)")
         kname = "scan launches of one hybrid step (content d=384 + CF r=50): " + kname
     else:
         flops = 2.0 * B * N_ITEMS * DIM
