@@ -356,3 +356,55 @@ def test_one_handle_two_streams(brickrec):
     for j, (sc, ids, cnt) in outs:
         assert np.array_equal(ids.cpu().numpy(), ref[j][1])
         assert np.array_equal(sc.cpu().numpy(), ref[j][0])
+
+
+def _bf16_operand(a):
+    """What a bf16 index stores / a bf16 query becomes: f64 norm, f32 quotient, RNE -> bf16."""
+    import torch
+    a64 = a.astype(np.float64)
+    nrm = np.sqrt((a64 * a64).sum(1, keepdims=True))
+    nrm[nrm == 0] = 1.0
+    f = (a64 / nrm).astype(np.float32)
+    return torch.from_numpy(f).to(torch.bfloat16).float().numpy().astype(np.float64)
+
+
+@pytest.mark.parametrize("dtype,d,B", [
+    ("f32", 500, 64),     # exact re-rank path at its widest operand (Dpad_b 512), scan2
+    ("f32", 500, 600),    # the same on scan4 (query chunks > 256 rows, one-wave select)
+    ("f32", 1000, 40),    # wider than the re-rank / split scans: the tiled gemm_nt fallback
+    ("bf16", 768, 300),   # bf16 scan4 at d = 768 (the configs[3] row width), slab path
+    ("bf16", 1000, 40),   # bf16 wider than scan4 takes: the tiled gemm_nt fallback
+])
+def test_row_widths_beyond_the_configs(brickrec, dtype, d, B):
+    """Every scan / fallback path picked by the row width, semantic and similar + mask, vs the
+    oracle (f32: exact cosine; bf16: the device's own bf16 operands, f32 accumulate)."""
+    n, k = 6000, 30
+    x = R.unit_rows(n, d, 21 + d)
+    q = R.unit_rows(B, d, 22 + d)
+    idx = brickrec.ItemIndex(dtype=dtype)
+    idx.upload_items(x)
+    sc, ids, cnt = idx.search("semantic", k, q_rows=q)
+    if dtype == "f32":
+        sim = R.cosine_scores(q, x).astype(np.float64)
+    else:
+        sim = _bf16_operand(q) @ _bf16_operand(x).T
+    gate = Gate(f"{dtype} {n} x {d} semantic B={B}")
+    for i in range(B):
+        ri, rs = R.topk_indices(sim[i], k + 1)
+        check_row(gate, sc[i], ids[i], ri[:k], rs[:k], k, rs[k])
+    gate.report(0.1)
+    rng = np.random.default_rng(d)
+    mask = rng.random(n) < 0.3
+    qi = rng.choice(n, min(B, 32), replace=False)
+    sc, ids, cnt = idx.search("similar", k, q_items=qi, mask=mask)
+    xs = x.astype(np.float64) if dtype == "f32" else _bf16_operand(x)
+    if dtype == "f32":
+        xs = xs / np.linalg.norm(xs, axis=1, keepdims=True)
+    gate = Gate(f"{dtype} {n} x {d} similar + mask")
+    for j, r in enumerate(qi):
+        s = xs @ xs[r]
+        order = np.lexsort((np.arange(n), -s))      # (score desc, id asc); rank 0 dropped
+        order = order[1:]
+        order = order[mask[order]]
+        check_row(gate, sc[j], ids[j], order[:k], s[order[:k]], k, s[order[k]])
+    gate.report(0.1)
