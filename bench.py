@@ -307,23 +307,30 @@ def run_sharded(args, rank, world, local, dev):
     dist.destroy_process_group()
 
 
-def make_lane(brickrec, workload, x, B, local, dev, rank, j, dtype, inflight, extra):
-    """One in-flight lane: its own index handle (own HIP stream + workspace) and batch."""
-    import torch
+def make_base(brickrec, workload, x, local, dtype, extra):
+    """The resident index of this GPU: one copy of the rows (and CF factors / attributes)."""
     idx = brickrec.ItemIndex(device=local, dtype=dtype)
     idx.upload_items(x)
+    if workload == "c3":
+        idx.upload_cf(extra["f"])
+        idx.upload_attrs(extra["parts"], extra["year"], extra["theme"])
+    return idx
+
+
+def make_lane(brickrec, workload, base, B, local, dev, rank, j, inflight, extra):
+    """One in-flight lane: a view of the resident index (own HIP stream + workspace, shared rows,
+    bb_create_view) and its own batch."""
+    import torch
+    idx = base.view()
     s = torch.cuda.current_stream(dev) if inflight == 1 else torch.cuda.Stream(dev)
     if workload == "c3":
-        f, parts, year, theme = extra["f"], extra["parts"], extra["year"], extra["theme"]
-        idx.upload_cf(f)
-        idx.upload_attrs(parts, year, theme)
         mask = idx.eval_mask(brickrec.Predicate(parts_max=800, year_min=2015))
         rng = np.random.default_rng(7000 + rank + 10 * j)
         liked = rng.choice(N_ITEMS, B, replace=False)
         rated = np.zeros((B, N_ITEMS), bool)
         for b in range(B):
             rated[b, rng.choice(N_ITEMS, int(rng.integers(10, 31)), replace=False)] = True
-        u = rng.normal(0.0, 0.1, (B, f.shape[1])).astype(np.float32)
+        u = rng.normal(0.0, 0.1, (B, extra["f"].shape[1])).astype(np.float32)
         mw = torch.from_numpy(brickrec.bits_from_bool(mask).view(np.int32)).to(dev)
         ew = torch.from_numpy(brickrec.bits_from_bool(rated).view(np.int32)).to(dev)
         run, outs = idx.prepared_search("hybrid", TOPK, q_items=torch.from_numpy(liked).to(dev),
@@ -334,7 +341,7 @@ def make_lane(brickrec, workload, x, B, local, dev, rank, j, dtype, inflight, ex
     return idx, s, run, outs, q
 
 
-def gpu_batch_sweep(brickrec, x, local, dev, dtype, seconds=0.5):
+def gpu_batch_sweep(brickrec, base, local, dev, seconds=0.5):
     """GPU q/s (3 in flight) and serial p50 at B ∈ {1 (top-10), 256, 1024, 4096}: the
     north_star's batch axis at 25K items."""
     import torch
@@ -342,8 +349,7 @@ def gpu_batch_sweep(brickrec, x, local, dev, dtype, seconds=0.5):
     for b, kk in ((1, 10), (256, 50), (1024, 50), (4096, 50)):
         lanes = []
         for j in range(3):
-            idx = brickrec.ItemIndex(device=local, dtype=dtype)
-            idx.upload_items(x)
+            idx = base.view()
             q = unit_rows_torch(b, DIM, 555 + j, dev)
             s = torch.cuda.Stream(dev)
             run, _ = idx.prepared_search("semantic", kk, q_rows=q, stream=s)
@@ -385,6 +391,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-sweep", action="store_true", help="skip the GPU batch sweep")
     ap.add_argument("--inflight", type=int, default=3, help="batches in flight per GPU (1 = strictly serial)")
+    ap.add_argument("--lane-copies", action="store_true", help="one uploaded copy of the rows per in-flight lane")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2 = configs[1] (default line); c3 = configs[2] hybrid; c4 / c5 = the sharded configs[3] / [4]")
     args = ap.parse_args()
@@ -412,10 +419,14 @@ def main():
                  "parts": rng.integers(1, 6000, N_ITEMS).astype(np.int32),
                  "year": rng.integers(1949, 2025, N_ITEMS).astype(np.int16),
                  "theme": rng.integers(0, 400, N_ITEMS).astype(np.int32)}
-    # `inflight` batches in flight: each lane is its own index handle (own HIP stream,
-    # workspace and 39 MB item copy) serving its own batch; consecutive steps alternate
-    # lanes, so one batch's latency-bound select overlaps the next batch's MFMA scan.
-    lanes = [make_lane(brickrec, args.workload, x, B, local, dev, rank, j, args.dtype, args.inflight, extra)
+    # `inflight` batches in flight: each lane is a view of one resident index (own HIP
+    # stream and workspace, the rows shared) serving its own batch; consecutive steps
+    # alternate lanes, so one batch's latency-bound select overlaps the next batch's scan.
+    base = make_base(brickrec, args.workload, x, local, args.dtype, extra)
+    # (--lane-copies: every lane uploads its own copy of the rows — the round-1 scheme, A/B runs)
+    lanes = [make_lane(brickrec, args.workload,
+                       make_base(brickrec, args.workload, x, local, args.dtype, extra) if args.lane_copies else base,
+                       B, local, dev, rank, j, args.inflight, extra)
              for j in range(args.inflight)]
     idx, stream, run, (o_sc, o_ids, o_cnt), q = lanes[0]
 
@@ -527,7 +538,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_sweep and not hybrid:
-        out["gpu_batch_sweep"] = gpu_batch_sweep(brickrec, x, local, dev, args.dtype)
+        out["gpu_batch_sweep"] = gpu_batch_sweep(brickrec, base, local, dev)
     if rank == 0 and world == 1 and not args.no_cpu and not hybrid:
         x_np = x.cpu().numpy()
         q_np = q.cpu().numpy()

@@ -91,10 +91,31 @@ class ItemIndex:
         self.r = 0
 
     # ------------------------------------------------------------------ lifetime
+    def view(self) -> "ItemIndex":
+        """A second handle over this index's resident rows (bb_create_view): its own HIP stream
+        and workspace, no second copy of the items — for keeping several batches in flight.
+        Close the views before closing or re-uploading this index."""
+        v = ItemIndex.__new__(ItemIndex)
+        v._lib, v.dtype, v.device, v.id_offset = self._lib, self.dtype, self.device, self.id_offset
+        h = C.c_void_p()
+        with self._mu:
+            L.check(self._lib.bb_create_view(self._h, C.byref(h)), "bb_create_view")
+        v._h = h
+        v._mu = threading.Lock()
+        v.n_items, v.d, v.r = self.n_items, self.d, self.r
+        v._base = self  # keeps the base alive while the view is
+        self._views = getattr(self, "_views", 0) + 1
+        return v
+
     def close(self):
         if getattr(self, "_h", None):
-            self._lib.bb_destroy(self._h)
+            base = getattr(self, "_base", None)
+            if getattr(self, "_views", 0):
+                raise L.BrickrecError("close this index's views first")
+            L.check(self._lib.bb_destroy(self._h), "bb_destroy")
             self._h = None
+            if base is not None:
+                base._views -= 1
 
     def __del__(self):
         try:

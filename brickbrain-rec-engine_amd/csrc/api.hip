@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -47,8 +48,10 @@ const char* kFamNames[K_NFAM] = {"prep", "gemm", "select", "finalize", "mask", "
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  bool owned = true;  // false: an alias of another handle's buffer (bb_create_view)
   int ensure(size_t bytes) {
     if (bytes <= cap) return BB_OK;
+    if (!owned) return fail(BB_E_STATE, "a view cannot resize its base's buffers");
     if (p) {
       hipError_t e = hipFree(p);
       if (e != hipSuccess) return fail(BB_E_HIP, std::string("hipFree: ") + hipGetErrorString(e));
@@ -64,9 +67,10 @@ struct DevBuf {
     return BB_OK;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p && owned) (void)hipFree(p);
     p = nullptr;
     cap = 0;
+    owned = true;
   }
 };
 
@@ -81,6 +85,8 @@ struct bb_index {
   int stream_opt = -1;                 // BB_OPT_STREAM
   int64_t stream_min_items = 100000;   // BB_OPT_STREAM_MIN_ITEMS
   int refine_opt = -1;                 // BB_OPT_STREAM_REFINE
+  bb_index* base = nullptr;            // a view (bb_create_view): the handle owning the rows
+  std::atomic<int> n_views{0};         // views of this handle still alive
   hipStream_t stream = nullptr;
   std::mutex mu;
   // Cross-stream ordering of the shared workspace: every call records `done` on the stream it
@@ -259,8 +265,49 @@ int bb_create(const bb_desc* desc, bb_index** out) {
   return BB_OK;
 }
 
+int bb_create_view(bb_index* b, bb_index** out) {
+  if (!b || !out) return fail(BB_E_ARG, "bb_create_view: null argument");
+  *out = nullptr;
+  if (b->base) return fail(BB_E_ARG, "bb_create_view: the base is itself a view");
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  BB_HIP(hipStreamSynchronize(b->stream));  // the base's uploads are complete
+  bb_desc desc{b->device, b->dtype, b->id_offset, b->ws_set ? b->ws_cap : 0};
+  bb_index* x = nullptr;
+  int rc = bb_create(&desc, &x);
+  if (rc) return rc;
+  x->stream_opt = b->stream_opt;
+  x->stream_min_items = b->stream_min_items;
+  x->refine_opt = b->refine_opt;
+  x->n = b->n;
+  x->Npad = b->Npad;
+  x->d = b->d;
+  x->Dpad = b->Dpad;
+  x->r = b->r;
+  x->Rpad = b->Rpad;
+  x->Dpad_b = b->Dpad_b;
+  x->Rpad_b = b->Rpad_b;
+  for (auto pr : {std::make_pair(&x->items, &b->items), std::make_pair(&x->items_present, &b->items_present),
+                  std::make_pair(&x->ones, &b->ones), std::make_pair(&x->zeros, &b->zeros),
+                  std::make_pair(&x->cf, &b->cf), std::make_pair(&x->cf_present, &b->cf_present),
+                  std::make_pair(&x->items3, &b->items3), std::make_pair(&x->cf3, &b->cf3),
+                  std::make_pair(&x->items_bf, &b->items_bf), std::make_pair(&x->cf_bf, &b->cf_bf),
+                  std::make_pair(&x->rr_stats, &b->rr_stats), std::make_pair(&x->parts, &b->parts),
+                  std::make_pair(&x->year, &b->year), std::make_pair(&x->theme, &b->theme)}) {
+    pr.first->p = pr.second->p;
+    pr.first->cap = pr.second->cap;
+    pr.first->owned = false;
+  }
+  x->base = b;
+  ++b->n_views;
+  *out = x;
+  return BB_OK;
+}
+
 int bb_destroy(bb_index* x) {
   if (!x) return BB_OK;
+  if (x->n_views > 0) return fail(BB_E_STATE, "bb_destroy: destroy the index's views first");
+  if (x->base) --x->base->n_views;
   {
     DeviceGuard g(x->device);
     (void)hipStreamSynchronize(x->stream);
@@ -388,6 +435,8 @@ static int make_rr(bb_index* x, DevBuf& rows, DevBuf& bf, int ld, int& ld_b, int
 
 int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t in_dtype, int32_t prenormalized,
                     int32_t where, const uint32_t* present_bits) {
+  if (x && x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
+  if (x && x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
   if (!x || !rows || n <= 0 || d <= 0) return fail(BB_E_ARG, "bb_upload_items: bad arguments");
   if (in_dtype != F32 && in_dtype != BF16 && in_dtype != F64) return fail(BB_E_ARG, "bad input dtype");
   if (n >= 0xFFFFFFFFll - x->id_offset) return fail(BB_E_ARG, "too many items for 32-bit ids");
@@ -421,6 +470,8 @@ int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t
 }
 
 int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const uint32_t* present_bits) {
+  if (x && x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
+  if (x && x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
   if (!x || !f || r <= 0) return fail(BB_E_ARG, "bb_upload_cf: bad arguments");
   if (x->n <= 0) return fail(BB_E_STATE, "upload items before CF factors");
   std::lock_guard<std::mutex> lk(x->mu);
@@ -448,6 +499,8 @@ int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const 
 }
 
 int bb_upload_attrs(bb_index* x, const int32_t* num_parts, const int16_t* year, const int32_t* theme_id) {
+  if (x && x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
+  if (x && x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
   if (!x || !num_parts || !year || !theme_id) return fail(BB_E_ARG, "bb_upload_attrs: bad arguments");
   if (x->n <= 0) return fail(BB_E_STATE, "upload items before attributes");
   std::lock_guard<std::mutex> lk(x->mu);

@@ -208,6 +208,13 @@ int bb_set_option(bb_index* idx, int32_t option, int64_t value);
  * read on the index's own stream, so they must be complete when the call is made. */
 int bb_get_rows(bb_index* idx, const int64_t* ids, int32_t B, void* out, int32_t where);
 
+/* A second handle over the same resident rows (no reference counterpart: serving plumbing).
+ * The view has its own HIP stream and scratch workspace but aliases the base's item rows, CF
+ * factors, attribute columns and bitsets, so several batches can be in flight on one device
+ * with ONE copy of the index in HBM / the MALL instead of one per in-flight handle.  Uploads to
+ * a view, or to a base while it has views, fail with BB_E_STATE; destroy the views first. */
+int bb_create_view(bb_index* base, bb_index** out);
+
 int bb_info(bb_index* idx, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* r);
 int bb_destroy(bb_index* idx);
 const char* bb_last_error(void);

@@ -408,3 +408,58 @@ def test_row_widths_beyond_the_configs(brickrec, dtype, d, B):
         order = order[mask[order]]
         check_row(gate, sc[j], ids[j], order[:k], s[order[:k]], k, s[order[k]])
     gate.report(0.1)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_views_share_the_resident_rows(brickrec, dtype):
+    """bb_create_view: three views of one resident index serve batches in flight on their own
+    streams (semantic, and hybrid with CF + mask + exclusions); every result equals the base
+    handle's own result for the same batch.  Uploads to a view, re-uploads to a base with live
+    views, and closing a base before its views are refused."""
+    import torch
+    n, d, r, B, k = 25216, 384, 50, 300, 50
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(41)
+    x = R.unit_rows(n, d, 1234)
+    f = rng.normal(0.0, 0.1, (n, r)).astype(np.float32)
+    base = brickrec.ItemIndex(dtype=dtype)
+    base.upload_items(torch.from_numpy(x).to(dev))
+    base.upload_cf(f)
+    mask = rng.random(n) < 0.4
+    views = [base.view() for _ in range(3)]
+    jobs = []
+    for j, v in enumerate(views):
+        q = torch.from_numpy(R.unit_rows(B, d, 60 + j)).to(dev)
+        liked = rng.choice(n, B, replace=False)
+        u = rng.normal(0.0, 0.1, (B, r)).astype(np.float32)
+        rated = np.zeros((B, n), bool)
+        for b in range(B):
+            rated[b, rng.choice(n, 20, replace=False)] = True
+        s = torch.cuda.Stream(dev)
+        run_s, out_s = v.prepared_search("semantic", k, q_rows=q, stream=s)
+        run_h, out_h = v.prepared_search("hybrid", k, q_items=torch.from_numpy(liked).to(dev),
+                                         q_cf=torch.from_numpy(u).to(dev),
+                                         mask=torch.from_numpy(brickrec.bits_from_bool(mask).view(np.int32)).to(dev),
+                                         excl=torch.from_numpy(brickrec.bits_from_bool(rated).view(np.int32)).to(dev),
+                                         stream=s)
+        jobs.append((run_s, out_s, run_h, out_h, q.cpu().numpy(), liked, u, rated))
+    for _ in range(3):
+        for run_s, _, run_h, _, *_ in jobs:
+            run_s()
+            run_h()
+    torch.cuda.synchronize()
+    for run_s, (sc, ids, cnt), run_h, (hsc, hids, hcnt), q, liked, u, rated in jobs:
+        rs, ri, _ = base.search("semantic", k, q_rows=q)
+        assert np.array_equal(ids.cpu().numpy(), ri) and np.array_equal(sc.cpu().numpy(), rs)
+        rs, ri, _ = base.search("hybrid", k, q_items=liked, q_cf=u, mask=mask, excl=rated)
+        assert np.array_equal(hids.cpu().numpy(), ri) and np.array_equal(hsc.cpu().numpy(), rs)
+    with pytest.raises(brickrec.BrickrecError):
+        views[0].upload_items(x)
+    with pytest.raises(brickrec.BrickrecError):
+        base.upload_cf(f)
+    with pytest.raises(brickrec.BrickrecError):
+        base.close()
+    for v in views:
+        v.close()
+    base.upload_cf(f)   # no views left: allowed again
+    base.close()
