@@ -1166,7 +1166,33 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     fa.ids = o_id + (size_t)b0 * q->k;
     fa.counts = o_cnt ? o_cnt + b0 : nullptr;
     fa.n_rows = bc;
+    static const bool fin_trace = getenv("BB_SELECT_TRACE") != nullptr;
+    if (fin_trace) {
+      if ((rc = x->trace.ensure((size_t)bc * 8 * 8))) return rc;
+      BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 64, s));
+      fa.trace = (uint64_t*)x->trace.p;
+    }
     if ((rc = timed(x, K_FIN, s, [&] { return launch_finalize(fa, s); }))) return rc;
+    if (fin_trace) {  // finalize phases: keys loaded, table ready, content blended, CF-only, end
+      std::vector<uint64_t> tr((size_t)bc * 8);
+      BB_HIP(hipMemcpyAsync(tr.data(), x->trace.p, tr.size() * 8, hipMemcpyDeviceToHost, s));
+      BB_HIP(hipStreamSynchronize(s));
+      double acc[8] = {0};
+      uint64_t t0 = ~0ull, t1 = 0;
+      int rows = 0;
+      for (int i = 0; i < bc; ++i) {
+        const uint64_t* t = &tr[(size_t)i * 8];
+        if (!t[5] || !t[4]) continue;
+        ++rows;
+        for (int j = 1; j < 6; ++j) acc[j] += (double)(t[j] - t[0]);
+        t0 = std::min(t0, t[0]);
+        t1 = std::max(t1, t[5]);
+      }
+      rows = std::max(rows, 1);
+      fprintf(stderr, "[bb finalize trace] rows=%d us-from-start: keys %.2f table %.2f content %.2f cf-only %.2f end %.2f  "
+              "span %.2f us\n", rows, acc[1] / rows / 100, acc[2] / rows / 100, acc[3] / rows / 100, acc[4] / rows / 100,
+              acc[5] / rows / 100, (double)(t1 - t0) / 100);
+    }
   }
   if (stream) {
     // a candidate region overflowed (masses of equal scores, a pilot sample unlike the rest):

@@ -253,6 +253,7 @@ struct FinalizeArgs {
   float* scores;            // [B][k]
   int64_t* ids;             // [B][k]
   int32_t* counts;          // [B] or null
+  uint64_t* trace;          // probe runs (BB_SELECT_TRACE): per-row phase stamps, or null
 };
 
 struct PrepArgs {

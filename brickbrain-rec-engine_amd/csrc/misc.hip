@@ -397,6 +397,10 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
   __shared__ uint32_t eg[2 * kMaxKInt];
   __shared__ int nnz[2], n_ent;
   const int q = blockIdx.x, tid = threadIdx.x;
+  auto stamp = [&](int slot) {  // probe-only phase timeline (s_memrealtime, 100 MHz)
+    if (a.trace && tid == 0) a.trace[q * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   if (tid < 2) nnz[tid] = 0;
   if (tid == 0) n_ent = 0;
   __syncthreads();
@@ -410,6 +414,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
   for (int side = 0; side < a.sides; ++side)
     if (cnt_local[side]) atomicAdd(&nnz[side], cnt_local[side]);
   __syncthreads();
+  stamp(1);
   int start[2] = {0, 0}, c[2] = {0, 0};
   for (int side = 0; side < a.sides; ++side) {
     const uint64_t head = lst[side][0];
@@ -448,6 +453,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
   for (int i = tid; i < kTab; i += kFinThreads) tab_g[i] = 0u;
   for (int j = tid; j < c[1]; j += kFinThreads) used[j] = 0;
   __syncthreads();
+  stamp(2);
   auto slot0 = [](uint32_t g) { return (int)((g * 2654435761u) >> 22) & (kTab - 1); };
   for (int j = tid; j < c[1]; j += kFinThreads) {
     const uint32_t g = gid_of(L1[j]);
@@ -477,6 +483,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
     eg[i] = g;
   }
   __syncthreads();
+  stamp(3);
   for (int j = tid; j < c[1]; j += kFinThreads) {
     const uint32_t g = gid_of(L1[j]);
     if (!used[j]) {
@@ -487,14 +494,28 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
     }
   }
   __syncthreads();
+  stamp(4);
   const int ne = c[0] + n_ent;
   const int n = ne < a.k ? ne : a.k;
+  // output position = rank under (h desc, id asc): 16 entries per round, every LDS read of a
+  // round issued before any compare (one read latency per entry took 15.6 of the kernel's
+  // 22 us at configs[2]; a bitonic network over the padded entries, 12 us, r02m trace)
   for (int e = tid; e < ne; e += kFinThreads) {
     const uint64_t hk = ek[e];
     const uint32_t g = eg[e];
-    int rank = 0;
-#pragma unroll 8
-    for (int f = 0; f < ne; ++f) rank += (ek[f] > hk) || (ek[f] == hk && eg[f] < g);
+    int rank = 0, f = 0;
+    for (; f + 16 <= ne; f += 16) {
+      uint64_t kk[16];
+      uint32_t gg[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        kk[j] = ek[f + j];
+        gg[j] = eg[f + j];
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) rank += (kk[j] > hk) || (kk[j] == hk && gg[j] < g);
+    }
+    for (; f < ne; ++f) rank += (ek[f] > hk) || (ek[f] == hk && eg[f] < g);
     if (rank < a.k) {
       sc[rank] = (float)eh[e];
       id[rank] = (int64_t)g;
@@ -505,6 +526,8 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
     id[i] = -1;
   }
   if (a.counts && tid == 0) a.counts[q] = n;
+  __syncthreads();
+  stamp(5);
 }
 
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
