@@ -905,7 +905,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         ga.excl = has_excl ? (const uint32_t*)d_excl + (size_t)b0 * nw : (const uint32_t*)x->zeros.p;
         ga.excl_ld = has_excl ? nw : 0;
         ga.tmax = (uint32_t*)x->tmax.p + (dual && side ? (size_t)Bc * ldt * 2 : 0);
-        ga.pmax = ga.tmax + (size_t)Bc * ldt;
+        // present maxima only where a rank 0 is dropped (the content side of similar / hybrid):
+        // the scans skip the half-wave of maxima stores otherwise (the dual scan always
+        // stores both: a uniform store measured 2.6% faster there than the masked one)
+        ga.pmax = side_drop || dual ? ga.tmax + (size_t)Bc * ldt : nullptr;
         if (dual && side) ga.S = (float*)((int16_t*)x->S.p + (size_t)Bc * lds);  // the image's second half
         ga.ldt = ldt;
         int regions = 0, cand_cap = 0;

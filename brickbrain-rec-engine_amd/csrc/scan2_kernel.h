@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
             }
           } else if constexpr (s == 6) {
             if constexpr (epi && !(ABL & 16) && !STREAM) {
-              (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
+              if (!h || a.pmax) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
             }
           } else if constexpr (s == 7) {
             // as inline asm: a compiler-visible load would get a compiler wait before its
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
       else
         *(float4*)(a.S + e) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
     }
-    (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
+    if (!h || a.pmax) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
   };
 
   using EY = std::integral_constant<bool, true>;

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
               *(float4*)(Sblk + (size_t)ptile * 1024 + j * 256) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
             }
           } else if constexpr (s == 6) {
-            if constexpr (epi && !(ABL & 16) && !STREAM) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
+            if constexpr (epi && !(ABL & 16) && !STREAM) if (!h || a.pmax) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
           } else if constexpr (s == 7) {
             nw_p = a.present[w0 + tile];
             nw_m = a.mask[w0 + tile];
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan3_kernel(GemmArgs a, i
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       *(float4*)(Sblk + (size_t)tile * 1024 + j * 256) = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
-    (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
+    if (!h || a.pmax) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
   };
 
   using B0 = std::integral_constant<int, 0>;

@@ -128,7 +128,7 @@ constexpr int scan4_atA(int s, int U, int E, int pieces) {
 // ABL (tools/scan4_probe only): 1 = no epilogue, 2 = no staging after the first tile, 4 = no
 // per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no streaming
 // appends (compares only), 64 = streaming appends without their stores.
-template <int KU, int ABL = 0>
+template <int KU, int ABL = 0, bool PM = false>
 __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int tiles_total, int L) {
   typedef uint16_t T;
   constexpr int U = KU / 2;        // u-steps (one bf16 MFMA each) per tile and block
@@ -315,7 +315,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
           }
         }
       } else if constexpr (s == 6) {
-        if constexpr (!(ABL & 16)) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
+        if constexpr (!(ABL & 16)) if (PM || !h || a.pmax) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + ptile] = h ? tp : te;
       }
     }
   };
@@ -576,9 +576,9 @@ template <int KU0, int KU1, int ABL>
 __global__ __launch_bounds__(kScanWaves * 64, 1) void scan4_dual_kernel(GemmArgs a0, GemmArgs a1, int nc0, int t0,
                                                                         int nc1, int t1, int nb0) {
   if ((int)blockIdx.x < nb0)
-    scan4_body<KU0, ABL>(a0, nc0, t0, blockIdx.x);
+    scan4_body<KU0, ABL, true>(a0, nc0, t0, blockIdx.x);
   else
-    scan4_body<KU1, ABL>(a1, nc1, t1, blockIdx.x - nb0);
+    scan4_body<KU1, ABL, true>(a1, nc1, t1, blockIdx.x - nb0);
 }
 
 }  // namespace bb

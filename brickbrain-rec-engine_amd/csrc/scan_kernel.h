@@ -61,7 +61,7 @@ __device__ __forceinline__ void scan_epilogue(const GemmArgs& a, float* Srow, in
   te = te2 > te ? te2 : te;
   tp = tp2 > tp ? tp2 : tp;
   // one store instruction: the lower half writes tmax, the upper half pmax
-  (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
+  if (!h || a.pmax) (h ? a.pmax : a.tmax)[(size_t)q * a.ldt + tile] = h ? tp : te;
 }
 
 // KU = Kpad·sizeof(T)/16: 16-byte chunks per row (f32: 4 k-steps each; bf16: 1 MFMA each).
