@@ -1,9 +1,9 @@
 #!/bin/bash
-# select-phase traces (BB_SELECT_TRACE) of the re-rank selects at configs[1], B=1024/4096 and configs[2]
+# hardware-queue count vs in-flight depth at configs[1] (bench line without the CPU leg)
 set -u
 O=gpurun_out/r02r; mkdir -p $O
-for c in c2-B256 c2-B1024 c2-B4096 c3; do
-  BB_SELECT_TRACE=1 timeout -k 10 120 python3 tools/scale_bench.py --cases $c --seconds 0.2 > $O/$c.jsonl 2> $O/$c.err; rc=$?
-  echo "$c rc=$rc"; grep "trace" $O/$c.err | tail -4; [ $rc -ne 0 ] && { tail -5 $O/$c.err; exit $rc; }
-done
-exit 0
+for q in 4 8 16; do for L in 3 4 6 8; do
+  [ $q = 4 ] && [ $L -gt 4 ] && continue
+  timeout -k 10 200 env GPU_MAX_HW_QUEUES=$q python3 bench.py --no-cpu --no-sweep --inflight $L > $O/q${q}_l$L.log 2>&1 || { tail -3 $O/q${q}_l$L.log; exit 1; }
+  python3 -c "import json; d=json.loads(open('$O/q${q}_l$L.log').read().strip().splitlines()[-1]); print('q=$q L=$L', round(d['value']/1e6,3), 'M q/s', d['p50_ms'], d['p50_ms_serial'])"
+done; done

@@ -1,11 +1,7 @@
 #!/bin/bash
-# blocked scan2 image + int16 re-rank image: full GPU suite, then A/B of BB_S16 modes vs head lib
+# finalize1 phase trace at configs[2] (serial)
 set -u
 O=gpurun_out/r02u; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > $O/tests.log 2>&1; rc=$?
-echo "tests rc=$rc"; tail -3 $O/tests.log; [ $rc -ne 0 ] && exit $rc
-bash tools/gpu_ab_env.sh r02u_ab "BB_S16=2" "BB_S16=0" "HEAD" || exit 1
-for e in X=1 BB_S16=2 BB_S16=0; do
-  timeout -k 10 200 env $e python3 bench.py --workload c3 --steps 300 --no-cpu > $O/c3_$e.log 2>&1 || exit 1
-  python3 -c "import json; d=json.loads(open('$O/c3_$e.log').read().strip().splitlines()[-1]); print('c3 $e', round(d['value']/1e6,3), d['p50_ms_serial'], d['kernels_us_per_step'])"
-done
+BB_SELECT_TRACE=1 timeout -k 10 120 python3 tools/scale_bench.py --cases c3 --seconds 0.2 > $O/c3d.jsonl 2> $O/c3d.err || exit 1
+grep "finalize trace" $O/c3d.err | tail -3
+grep "select trace" $O/c3d.err | tail -3

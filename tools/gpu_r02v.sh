@@ -1,10 +1,16 @@
 #!/bin/bash
-# paired-halves blocked image: full GPU suite, A/B vs the session-start library, configs[2]
+# finalize1: one-wave register bitonic sort of the blended entries (ne <= 256) — GPU suite, phase trace, configs[2] A/B vs head
 set -u
-O=gpurun_out/r02v; mkdir -p $O
+O=gpurun_out/r02v2; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > $O/tests.log 2>&1; rc=$?
-echo "tests rc=$rc"; tail -3 $O/tests.log; [ $rc -ne 0 ] && exit $rc
-bash tools/gpu_ab_env.sh r02v_ab "HEAD" || exit 1
-timeout -k 10 200 python3 bench.py --workload c3 --steps 300 --no-cpu > $O/c3.log 2>&1 || exit 1
-python3 -c "import json; d=json.loads(open('$O/c3.log').read().strip().splitlines()[-1]); print('c3', round(d['value']/1e6,3), d['p50_ms_serial'], d['kernels_us_per_step'])"
-for f in $O/../r02v_ab/ab_*_1.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', d['kernels_us_per_step'])"; done
+echo "tests rc=$rc"; tail -1 $O/tests.log; [ $rc -ne 0 ] && exit $rc
+for lib in new head; do
+  if [ $lib = head ]; then L=BRICKREC_LIB=$(pwd)/tools/ab/libbrickrec_head.so; else L=X=1; fi
+  BB_SELECT_TRACE=1 timeout -k 10 120 env $L python3 tools/scale_bench.py --cases c3 --seconds 0.2 > $O/c3d_$lib.jsonl 2> $O/c3d_$lib.err || exit 1
+  echo "$lib: $(grep 'finalize trace' $O/c3d_$lib.err | tail -1)"
+done
+for rep in 1 2; do for lib in new head; do
+  if [ $lib = head ]; then L=BRICKREC_LIB=$(pwd)/tools/ab/libbrickrec_head.so; else L=X=1; fi
+  timeout -k 10 200 env $L python3 bench.py --workload c3 --steps 300 --no-cpu > $O/c3_${lib}_$rep.log 2>&1 || exit 1
+  python3 -c "import json; d=json.loads(open('$O/c3_${lib}_$rep.log').read().strip().splitlines()[-1]); print('c3 $lib', round(d['value']/1e6,3), d['p50_ms_serial'], d['kernels_us_per_step'])"
+done; done
