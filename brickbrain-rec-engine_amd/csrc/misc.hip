@@ -395,6 +395,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
   __shared__ double eh[2 * kMaxKInt];
   __shared__ uint64_t ek[2 * kMaxKInt];  // order image of eh (the legacy kernel's sort key)
   __shared__ uint32_t eg[2 * kMaxKInt];
+  __shared__ __attribute__((aligned(16))) uint32_t ehi[2 * kMaxKInt];  // order image of (float)eh
   __shared__ int nnz[2], n_ent;
   const int q = blockIdx.x, tid = threadIdx.x;
   auto stamp = [&](int slot) {  // probe-only phase timeline (s_memrealtime, 100 MHz)
@@ -480,6 +481,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
     const double fs = hit >= 0 ? (double)float_of_ord(ordk_of(L1[hit])) : 0.0;
     eh[i] = a.w_content * cs + a.w_cf * fs;
     ek[i] = ord64_of(eh[i]);
+    ehi[i] = ord_of((float)eh[i]);
     eg[i] = g;
   }
   __syncthreads();
@@ -490,6 +492,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
       const int pos = c[0] + atomicAdd(&n_ent, 1);
       eh[pos] = a.w_content * 0.0 + a.w_cf * (double)float_of_ord(ordk_of(L1[j]));
       ek[pos] = ord64_of(eh[pos]);
+      ehi[pos] = ord_of((float)eh[pos]);
       eg[pos] = g;
     }
   }
@@ -497,25 +500,47 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
   stamp(4);
   const int ne = c[0] + n_ent;
   const int n = ne < a.k ? ne : a.k;
-  // output position = rank under (h desc, id asc): 16 entries per round, every LDS read of a
-  // round issued before any compare (one read latency per entry took 15.6 of the kernel's
-  // 22 us at configs[2]; a bitonic network over the padded entries, 12 us, r02m trace)
+  // output position = rank under (h desc, id asc).  Counted on the order image of the f32
+  // rounding of h first (monotonic in h; 16 entries per round from four ds_read_b128
+  // broadcasts, two 32-bit compares each): entries above are better, below worse.  Only
+  // entries sharing that image with others (ties and near-ties, rare) take the full (h, id)
+  // comparison among them, batched the same way.  The
+  // full 96-bit count for every pair, with 32 LDS reads per round, took 9.5 us of the 21 us
+  // kernel at configs[2] (r02u trace).
   for (int e = tid; e < ne; e += kFinThreads) {
     const uint64_t hk = ek[e];
-    const uint32_t g = eg[e];
-    int rank = 0, f = 0;
+    const uint32_t g = eg[e], hh = ehi[e];
+    int gt = 0, ge = 0, f = 0;
     for (; f + 16 <= ne; f += 16) {
-      uint64_t kk[16];
-      uint32_t gg[16];
+      uint32_t kk[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *(uint4*)(kk + 4 * j) = *(const uint4*)(ehi + f + 4 * j);
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        kk[j] = ek[f + j];
-        gg[j] = eg[f + j];
+        gt += kk[j] > hh;
+        ge += kk[j] >= hh;
       }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) rank += (kk[j] > hk) || (kk[j] == hk && gg[j] < g);
     }
-    for (; f < ne; ++f) rank += (ek[f] > hk) || (ek[f] == hk && eg[f] < g);
+    for (; f < ne; ++f) {
+      gt += ehi[f] > hh;
+      ge += ehi[f] >= hh;
+    }
+    int rank = gt;
+    if (ge - gt > 1) {
+      for (f = 0; f + 16 <= ne; f += 16) {
+        uint32_t kk[16], gg[16];
+        uint64_t hv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          kk[j] = ehi[f + j];
+          hv[j] = ek[f + j];
+          gg[j] = eg[f + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) rank += kk[j] == hh && ((hv[j] > hk) || (hv[j] == hk && gg[j] < g));
+      }
+      for (; f < ne; ++f) rank += ehi[f] == hh && ((ek[f] > hk) || (ek[f] == hk && eg[f] < g));
+    }
     if (rank < a.k) {
       sc[rank] = (float)eh[e];
       id[rank] = (int64_t)g;

@@ -237,6 +237,35 @@ def test_ties_and_edges(brickrec):
     assert list(ids[0]) == list(range(10)) and np.all(sc[0] == 0)
 
 
+def test_hybrid_blend_ties(brickrec):
+    """Exact ties in the hybrid blend: every item row AND factor row has three copies, so
+    copies blend to the same h, which must come out id asc (recommendation_system.py:842 sorts
+    by score only; (h desc, id asc) is this build's fixed rule).  Drives finalize1's tie path:
+    its rank count resolves equal f32 images of h by the full (h, id) comparison."""
+    rng = np.random.default_rng(21)
+    nb, reps, d, r, B, k = 24, 4, 16, 8, 8, 10
+    base = rng.standard_normal((nb, d)).astype(np.float32)
+    fb = rng.standard_normal((nb, r)).astype(np.float32)
+    x, f = np.tile(base, (reps, 1)), np.tile(fb, (reps, 1))   # rows j, j + 24, j + 48, j + 72
+    n = x.shape[0]
+    u = rng.standard_normal((B, r)).astype(np.float32)
+    qi = np.arange(B) * 5
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(x)
+    idx.upload_cf(f)
+    sc, ids, cnt = idx.search("hybrid", k, q_items=qi, q_cf=u)
+    xb = R.normalize_rows(base.astype(np.float64))
+    for i in range(B):
+        cs = np.tile(xb[qi[i] % nb] @ xb.T, reps)   # copies score bit-identically
+        ok = np.ones(n, bool)
+        ok[int(np.argmax(cs))] = False               # rank 0: the lowest-id copy of the query
+        c_i, c_s = R.topk_indices(cs, 2 * k, ok)
+        f_i, f_s = R.topk_indices(np.tile(fb.astype(np.float64) @ u[i].astype(np.float64), reps), 2 * k)
+        ri, rsc = R.union_blend(c_i, c_s, f_i, f_s, 0.4, 0.6, k)
+        _check_lists(ids[i], sc[i], ri, rsc)
+        assert len(set(np.round(rsc, 9))) < len(rsc), "the case must hold blended ties"
+
+
 def test_bf16_index(brickrec):
     """bf16 MFMA path vs the oracle on the same bf16-rounded operands (f32 accumulate)."""
     import torch
