@@ -422,9 +422,11 @@ class ItemIndex:
     # ------------------------------------------------------------------ options
     def set_option(self, option: str, value: int):
         """Tuning knobs: "stream" (-1 auto / 0 off / 1 on), "stream_min_items", "workspace_bytes",
-        "stream_refine" (-1 auto / 0 off / 1 on: the two-level streaming bound)."""
+        "stream_refine" (-1 auto / 0 off / 1 on: the two-level streaming bound), "rr_lists" (-1 auto
+        / 0 off: bounded candidate lists instead of a score image on one-slab f32 searches)."""
         code = {"stream": L.BB_OPT_STREAM, "stream_min_items": L.BB_OPT_STREAM_MIN_ITEMS,
-                "workspace_bytes": L.BB_OPT_WORKSPACE_BYTES, "stream_refine": L.BB_OPT_STREAM_REFINE}[option]
+                "workspace_bytes": L.BB_OPT_WORKSPACE_BYTES, "stream_refine": L.BB_OPT_STREAM_REFINE,
+                "rr_lists": L.BB_OPT_RR_LISTS}[option]
         with self._mu:
             L.check(self._lib.bb_set_option(self._h, code, int(value)), "bb_set_option")
 

@@ -85,6 +85,7 @@ struct bb_index {
   int stream_opt = -1;                 // BB_OPT_STREAM
   int64_t stream_min_items = 100000;   // BB_OPT_STREAM_MIN_ITEMS
   int refine_opt = -1;                 // BB_OPT_STREAM_REFINE
+  int lists_opt = -1;                  // BB_OPT_RR_LISTS
   bb_index* base = nullptr;            // a view (bb_create_view): the handle owning the rows
   std::atomic<int> n_views{0};         // views of this handle still alive
   hipStream_t stream = nullptr;
@@ -119,6 +120,7 @@ struct bb_index {
   DevBuf trace;        // BB_SELECT_TRACE probe stamps
   DevBuf rr_flags;     // one-wave re-rank select: rows left to the block select
   DevBuf list1, max1;  // two-level streaming: exact top-K_int (+ rank-0 key) of items [0, n1)
+  DevBuf lists, r0lists;  // bounded candidate lists of the list scans (list_epi.h), both sides
   uint32_t* ovf_host = nullptr;  // pinned
 
   bool prof = false;
@@ -279,6 +281,7 @@ int bb_create_view(bb_index* b, bb_index** out) {
   x->stream_opt = b->stream_opt;
   x->stream_min_items = b->stream_min_items;
   x->refine_opt = b->refine_opt;
+  x->lists_opt = b->lists_opt;
   x->n = b->n;
   x->Npad = b->Npad;
   x->d = b->d;
@@ -319,7 +322,7 @@ int bb_destroy(bb_index* x) {
                       &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
                       &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
                       &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
-                      &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags})
+                      &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
     if (x->has_last) (void)hipEventSynchronize(x->done);
@@ -636,6 +639,22 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   static const bool no_rr = getenv("BB_NO_RR") != nullptr;
   const bool rr_c = !no_rr && !stream && n_slabs == 1 && need_content && x->items_bf.p;
   const bool rr_f = !no_rr && !stream && n_slabs == 1 && need_cf && x->cf_bf.p;
+  // Bounded candidate lists (list_epi.h, select_list.hip) on the re-rank scans: no score
+  // image; per lane the top-4 keys of every period of G tiles.  Geometry of a query chunk of
+  // bpad_c rows: item chunks of the scan launch, periods per chunk (enough lists that a list
+  // expects <= 1/3 of a top-K member: 2·chunks·periods >= 3·K_int), tiles per period.
+  auto list_geom = [&](int bpad_c, int& nch, int& np, int& G) -> bool {
+    if (x->lists_opt == 0 || scan4_used(BF16, bpad_c)) return false;
+    const int tiles = (int)(round_up(x->n, kTileRows) / 32);
+    nch = scan_n_chunks(bpad_c, tiles);
+    const int tpc = (tiles + nch - 1) / nch;
+    if (tpc > 2047 || nch > 256) return false;
+    np = 1;
+    while (2 * nch * np < 3 * K_int && 2 * nch * (np + 1) <= 1024 && np < tpc) ++np;
+    G = (tpc + np - 1) / np;
+    np = (tpc + G - 1) / G;
+    return 2 * nch * np <= 1024;
+  };
 
   // stage host inputs
   const size_t es_q = elem_size(q->q_dtype), es_cf = elem_size(q->q_cf_dtype);
@@ -794,8 +813,17 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // int16 score image on the re-rank scans (not with the fused re-rank prologue, whose
     // chunk-0 workgroups write the bound while the others already store scores)
     const bool s16_on = s16_env == 1 || (s16_env == 2 && scan4_used(BF16, bpad));
-    const bool s16_c = s16_on && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
-    const bool s16_f = s16_on && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
+    int l_nch = 0, l_np = 0, l_G = 0;
+    const bool lgeo = list_geom(bpad, l_nch, l_np, l_G);
+    const bool list_c = lgeo && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
+    const bool list_f = lgeo && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
+    const bool s16_c = !list_c && s16_on && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
+    const bool s16_f = !list_f && s16_on && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
+    const size_t list_side_b = (size_t)l_nch * l_np * (bpad / 32) * 64 * 16;
+    if ((list_c || list_f) &&
+        ((rc = x->lists.ensure(2 * list_side_b)) ||
+         (list_c && drop && (rc = x->r0lists.ensure((size_t)l_nch * (bpad / 32) * 64 * 8)))))
+      return rc;
     // the prep launches of both sides (hybrid) go out as one launch
     const bool prep_c = need_content && !fuse_c && !rrfuse_c, prep_f = need_cf && !fuse_f && !rrfuse_f;
     PrepArgs pa_c{}, pa_f{};
@@ -814,7 +842,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         pa.Dpad_f = x->Dpad;
         pa.eps_out = (float*)x->qeps.p;
         pa.istats = (const float*)x->rr_stats.p;
-        pa.h_out = s16_c ? (float*)x->qh.p : nullptr;
+        pa.h_out = s16_c || list_c ? (float*)x->qh.p : nullptr;
       }
       pa.items = x->items.p;
       pa.n_items = x->n;
@@ -843,7 +871,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         pa.Dpad_f = x->Rpad;
         pa.eps_out = (float*)x->qcfeps.p;
         pa.istats = (const float*)x->rr_stats.p + 4;
-        pa.h_out = s16_f ? (float*)x->qcfh.p : nullptr;
+        pa.h_out = s16_f || list_f ? (float*)x->qcfh.p : nullptr;
       }
       pa.src = (const char*)d_cf + (size_t)b0 * x->r * es_cf;
       pa.src_dtype = q->q_cf_dtype;
@@ -964,7 +992,14 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           ga.X = (const char*)(cf_side ? x->cf_bf.p : x->items_bf.p) + (size_t)c0 * w * 2;
           ga.ldx = ga.ldq = w;
           ga.Kpad = (int)w;
-          ga.s_h = (cf_side ? s16_f : s16_c) ? (const float*)(cf_side ? x->qcfh.p : x->qh.p) : nullptr;
+          ga.s_h = (cf_side ? s16_f || list_f : s16_c || list_c) ? (const float*)(cf_side ? x->qcfh.p : x->qh.p)
+                                                                   : nullptr;
+          if (cf_side ? list_f : list_c) {
+            ga.lists = (uint32_t*)((char*)x->lists.p + (side ? list_side_b : 0));
+            ga.r0lists = side_drop ? (uint32_t*)x->r0lists.p : nullptr;
+            ga.l_period = l_G;
+            ga.l_np = l_np;
+          }
           if (dual && side == 0) {
             ga_dual0 = ga;  // launched with side 1's
           } else if (dual) {
@@ -1053,6 +1088,26 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           sa.out_ids = o_id + (size_t)b0 * q->k;
           sa.out_counts = o_cnt ? o_cnt + b0 : nullptr;
           sa.k_final = q->k;
+        }
+        if (cf_side ? list_f : list_c) {
+          // bounded candidate lists: one select launch per search (both hybrid sides together)
+          sa.s_h = ga.s_h;
+          sa.lists = ga.lists;
+          sa.r0lists = ga.r0lists;
+          sa.l_chunks = l_nch;
+          sa.l_tiles = ncols_pad / 32;
+          sa.l_np = l_np;
+          sa.l_period = l_G;
+          sa.l_nb = bpad / 32;
+          final_pp = pp;
+          if (q->mode == BB_MODE_HYBRID && side == 0 && list_f) {
+            sa_dual0 = sa;  // launched with side 1's
+            continue;
+          }
+          const bool both = q->mode == BB_MODE_HYBRID && side == 1 && list_c;
+          if ((rc = timed(x, K_SELECT, s, [&] { return launch_select_list(both ? sa_dual0 : sa, both ? &sa : nullptr, bc, s); })))
+            return rc;
+          continue;
         }
         // BB_SELECT_TRACE (probe runs): per-phase s_memrealtime stamps of every query row,
         // averaged over the rows and printed to stderr
@@ -1318,6 +1373,10 @@ int bb_set_option(bb_index* x, int32_t option, int64_t value) {
     case BB_OPT_STREAM_REFINE:
       if (value < -1 || value > 1) return fail(BB_E_ARG, "BB_OPT_STREAM_REFINE must be -1, 0 or 1");
       x->refine_opt = (int)value;
+      return BB_OK;
+    case BB_OPT_RR_LISTS:
+      if (value < -1 || value > 1) return fail(BB_E_ARG, "BB_OPT_RR_LISTS must be -1, 0 or 1");
+      x->lists_opt = (int)value;
       return BB_OK;
     case BB_OPT_WORKSPACE_BYTES:
       if (value < (1ll << 20)) return fail(BB_E_ARG, "BB_OPT_WORKSPACE_BYTES must be >= 1 MiB");

@@ -91,9 +91,16 @@ struct GemmArgs {
   // slab costs 2 B per score; the select decodes c·s_h[q], whose bound ε (prep) covers it
   const float* s_h;         // [Mpad] quantum per query row
   float* q_h_out;           // fused re-rank prologue: writes the quantum beside q_eps_out
+  // bounded candidate lists (scan ABL & kScanList, list_epi.h): no score image; per lane the
+  // top-4 keys (u16 code of s / s_h[q], item position in the chunk) of every period of
+  // l_period tiles, and (r0lists set) the top-2 present half-tile maxima for rank 0
+  uint32_t* lists;          // uint4 at list_slot(chunk, period, l_np, Mpad/32, q >> 5, lane)
+  uint32_t* r0lists;        // uint2 at list_slot(chunk, 0, 1, Mpad/32, q >> 5, lane), or null
+  int32_t l_period, l_np;
 };
 constexpr int kScanStream = 512;  // scan ABL bit: streaming top-K epilogue
 constexpr int kScanS16 = 4096;    // scan ABL bit: int16 score image (GemmArgs.s_h)
+constexpr int kScanList = 8192;   // scan ABL bit: bounded candidate lists (GemmArgs.lists)
 
 // Quantum h of the int16 score image of one query and the widened bound of its decoded
 // scores.  |approximate score| <= |q̃|·Ñ_x·(1+γ) <= 16384·h, so no code saturates; the
@@ -215,6 +222,12 @@ struct SelectArgs {
   uint32_t* rr_flags;       // [B] or null
   // int16 score image (GemmArgs.s_h): S holds codes, score = code · s_h[row]; null = f32 S
   const float* s_h;
+  // bounded candidate lists of a kScanList scan (select_list_kernel): the scan's GemmArgs
+  // lists / r0lists and geometry (item chunks, tiles, periods per chunk, tiles per period,
+  // 32-query blocks); s_h = the code quantum h, rr_eps = ε'
+  const uint32_t* lists;
+  const uint32_t* r0lists;
+  int32_t l_chunks, l_tiles, l_np, l_period, l_nb;
 };
 constexpr int kRrCap = 512;
 constexpr int kRrR0Cap = 64;
@@ -314,6 +327,9 @@ hipError_t launch_rerank(const SelectArgs& a, int B, hipStream_t s);  // after l
 // one wave per query, one-slab re-rank searches (rr_flags set; rows it leaves: launch_select)
 hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s);
 hipError_t launch_select_rr_wave_dual(const SelectArgs& a0, const SelectArgs& a1, int B, hipStream_t s);
+// exact top-K of a kScanList scan (lists set, rr_* operands, one slab): one workgroup per row;
+// a1 != null: both sides of a hybrid search in one launch
+hipError_t launch_select_list(const SelectArgs& a0, const SelectArgs* a1, int B, hipStream_t s);
 hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s);

@@ -57,6 +57,11 @@ static void launch_scan_t(const GemmArgs& a, hipStream_t s) {
   // one workgroup per CU (LDS + VGPR budget): ~256 workgroups, chunks balanced to ±1 tile
   const int n_chunks = scan_n_chunks(a.Mpad, tiles);
   if constexpr (sizeof(T) == 2 && KU <= kRrMaxD / 8) {
+    if (a.lists) {  // exact re-rank path: bounded candidate lists
+      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanList>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
+                         n_chunks, tiles);
+      return;
+    }
     if (a.s_h && !a.cand) {  // exact re-rank path: int16 score image
       hipLaunchKernelGGL((scan2_kernel<T, KU, kScanS16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
                          n_chunks, tiles);
@@ -138,6 +143,10 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   // the int16 score image: bf16 scans of rows up to kRrMaxD, slab epilogue only
   if (a.s_h && (dtype != BF16 || a.cand || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.Kpad > kRrMaxD))
+    return hipErrorInvalidValue;
+  // candidate lists: the bf16 scan2 of a re-rank search (query chunks the scan4 does not take)
+  if (a.lists && (!a.s_h || a.q_istats || scan4_used(BF16, a.Mpad) || a.l_period <= 0 || a.l_np <= 0 ||
+                  (int64_t)a.l_period * a.l_np * scan_n_chunks(a.Mpad, a.Ncols / 32) < a.Ncols / 32))
     return hipErrorInvalidValue;
   if (gemm_uses_scan(dtype, a.Mpad, a.Kpad)) {
     if (dtype == BF16 ? launch_scan<uint16_t>(a, s) : launch_scan<float>(a, s)) return hipGetLastError();

@@ -15,6 +15,7 @@
 #pragma once
 #include <utility>
 
+#include "list_epi.h"
 #include "scan_kernel.h"
 
 namespace bb {
@@ -307,6 +308,13 @@ __device__ __forceinline__ void stream_end(const GemmArgs& a, size_t region, con
   if (a.cand_pmax) a.cand_pmax[region] = s.rkey;
 }
 
+// u-step of slice s of the list epilogue's S slices: spread evenly over u = 2 .. U-1
+constexpr int list_slice_u(int s, int S, int U) {
+  const int span = U > 3 ? U - 2 : 1;
+  const int u = 2 + s * span / S;
+  return u < U ? u : U - 1;
+}
+
 // ABL (tools/scan_probe only): 1 = no epilogue, 2 = no staging after the first tile,
 // 4 = no per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no
 // order-image / maxima arithmetic.
@@ -405,6 +413,30 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     sk = hq > 0.f ? 1.0f / (hq * 32767.f) : 0.f;
     asm volatile("" : "+v"(sk));  // consumed before any LDS-DMA is in flight
   }
+  // bounded candidate lists (list_epi.h): code scale k2 = 1/(65535·h), the lane's top-4 of
+  // the current period, the rank-0 top-2, the period counters (wave-uniform)
+  constexpr bool LIST = (ABL & kScanList) != 0 && !STREAM && !S16;
+  float k2 = 0.f;
+  if constexpr (LIST) {
+    const float hq = q < a.M_valid ? a.s_h[q] : 0.f;
+    k2 = hq > 0.f ? 1.0f / (hq * 65535.f) : 0.f;
+    asm volatile("" : "+v"(k2));  // consumed before any LDS-DMA is in flight
+  }
+  ListTop4 lst;
+  ListTop2 r0l;
+  uint32_t l_e16 = 0, l_pb2 = 0, l_kodd = 0;
+  bool l_full = true;
+  int l_cnt = 0, l_period = 0;
+  const int l_nb = a.Mpad >> 5, l_blk = q >> 5;
+  const bool l_live = __any(q < a.M_valid);  // padded query blocks store nothing
+  auto list_store = [&]() __attribute__((always_inline)) {
+    if (l_live)
+      *(uint4*)(a.lists + 4 * list_slot(chunk, l_period, a.l_np, l_nb, l_blk, lane)) =
+          make_uint4(lst.k0, lst.k1, lst.k2, lst.k3);
+    lst.reset();
+    l_cnt = 0;
+    ++l_period;
+  };
   StreamLane sl;
   const size_t region = ((size_t)q * n_chunks + chunk) * 2 + h;
   if constexpr (STREAM) stream_begin(a, q, region, sl);
@@ -471,6 +503,57 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
           asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[u]));
       }
       if constexpr (u > 0) asm volatile("" ::"v"(__builtin_bit_cast(u32x4v, fq[(u + 3) % 4])));
+      // ---- list epilogue (kScanList): eligibility, 16 half-pair slices (codes, keys, top-4
+      // inserts), rank 0, the period store, then the next tile's words and staging ----
+      if constexpr (LIST) {
+        constexpr int kLS = 20 + PIECES;
+        static_for<kLS>([&](auto SS) {
+          constexpr int s = decltype(SS)::value;
+          if constexpr (list_slice_u(s, kLS, U) == u) {
+            if constexpr (s == 0) {
+              if constexpr (epi) {
+                l_e16 = list_elig16(pw & mw & ~ew, ptile0, a.n_valid, h);
+                l_full = __all(l_e16 == 0xFFFFu);
+                l_pb2 = ((uint32_t)(((ptile - tile_lo) << 5) | (h << 2))) * 0x10001u;
+              }
+            } else if constexpr (s <= 16) {
+              if constexpr (epi) {
+                constexpr int pp = (s - 1) >> 1;
+                if constexpr (((s - 1) & 1) == 0) {
+                  uint32_t w = list_codes(p[2 * pp], p[2 * pp + 1], k2);
+                  if (!l_full) {
+                    const uint32_t lo = 0u - ((l_e16 >> (2 * pp)) & 1u), hi = 0u - ((l_e16 >> (2 * pp + 1)) & 1u);
+                    w &= (lo & 0xFFFFu) | (hi & 0xFFFF0000u);
+                  }
+                  const uint32_t ix = l_pb2 + list_pair_pos(pp);
+                  lst.ins(__builtin_amdgcn_perm(w, ix, 0x05040100u));
+                  l_kodd = __builtin_amdgcn_perm(w, ix, 0x07060302u);
+                } else {
+                  lst.ins(l_kodd);
+                }
+              }
+            } else if constexpr (s == 17) {
+              if constexpr (epi) {
+                if (a.r0lists) {
+                  const float m = list_present_max(p, list_elig16(pw, ptile0, a.n_valid, h));
+                  r0l.ins(list_r0_key(m, k2, (uint32_t)(ptile - tile_lo)));
+                }
+              }
+            } else if constexpr (s == 18) {
+              if constexpr (epi) {
+                if (++l_cnt == a.l_period) list_store();
+              }
+            } else if constexpr (s == 19) {
+              asm volatile("global_load_dword %0, %1, off" : "=v"(nw_p) : "v"(a.present + w0 + tile) : "memory");
+              asm volatile("global_load_dword %0, %1, off" : "=v"(nw_m) : "v"(a.mask + w0 + tile) : "memory");
+              asm volatile("global_load_dword %0, %1, off" : "=v"(nw_e) : "v"(erow + w0 + tile) : "memory");
+            } else {
+              if constexpr (!(ABL & 2)) stage_piece(stile, sbuf, s - 20);
+            }
+          }
+        });
+        return;
+      }
       // ---- slices scheduled on this u-step: slice s runs at u = min(U-1, s+2) ----
       static_for<kEpiSlices>([&](auto SS) {
         constexpr int s = decltype(SS)::value;
@@ -543,6 +626,21 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   auto last_epilogue = [&](int tile, const f32x16s& p) __attribute__((always_inline)) {
     if constexpr (ABL & 1) return;
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15");  // asm-MFMA result -> VALU read
+    if constexpr (LIST) {
+      const uint32_t e16 = list_elig16(pw & mw & ~ew, tile * 32, a.n_valid, h);
+      const bool full = __all(e16 == 0xFFFFu);
+      const uint32_t pb2 = ((uint32_t)(((tile - tile_lo) << 5) | (h << 2))) * 0x10001u;
+#pragma unroll
+      for (int pp = 0; pp < 8; ++pp) list_pair(lst, p[2 * pp], p[2 * pp + 1], k2, pb2, pp, full, e16);
+      if (a.r0lists) {
+        const float m = list_present_max(p, list_elig16(pw, tile * 32, a.n_valid, h));
+        r0l.ins(list_r0_key(m, k2, (uint32_t)(tile - tile_lo)));
+        if (l_live)
+          *(uint2*)(a.r0lists + 2 * list_slot(chunk, 0, 1, l_nb, l_blk, lane)) = make_uint2(r0l.k0, r0l.k1);
+      }
+      list_store();  // the last (possibly partial) period
+      return;
+    }
     uint32_t te = 0, tp = 0;
     tile_maxima(p, tile * 32, a.n_valid, pw, pw & mw & ~ew, h, te, tp);
     if constexpr (STREAM) {

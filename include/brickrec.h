@@ -193,11 +193,16 @@ int bb_get_profile(bb_index* idx, bb_profile* out);
  *   BB_OPT_WORKSPACE_BYTES  score-slab workspace cap (default 512 MiB; streaming may use up
  *                           to 4 GiB unless this is set)
  *   BB_OPT_STREAM_REFINE    -1 auto (default), 0 never, 1 always (index >= 2x the pilot): the
- *                           two-level streaming bound.  Results are identical either way. */
+ *                           two-level streaming bound.  Results are identical either way.
+ *   BB_OPT_RR_LISTS         -1 auto (default, = 1), 0 off: one-slab searches of an f32 index
+ *                           keep bounded per-lane candidate lists in the scan instead of
+ *                           writing a score image for the select (no B×n image).  Results are
+ *                           identical either way. */
 #define BB_OPT_STREAM 1
 #define BB_OPT_STREAM_MIN_ITEMS 2
 #define BB_OPT_WORKSPACE_BYTES 3
 #define BB_OPT_STREAM_REFINE 4
+#define BB_OPT_RR_LISTS 5
 int bb_set_option(bb_index* idx, int32_t option, int64_t value);
 
 /* Stored (normalised, index-dtype) item rows of B global ids into out (B×d, row-major;

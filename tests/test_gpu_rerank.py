@@ -214,3 +214,36 @@ np.savez(sys.argv[3], sc=sc, ids=ids, s2=s2, i2=i2)
         out[fused] = np.load(path)
     for key in ("sc", "ids", "s2", "i2"):
         assert np.array_equal(out["0"][key], out["1"][key]), key
+
+
+def test_rr_lists_vs_image_identical(brickrec):
+    """The bounded candidate lists (BB_OPT_RR_LISTS, default on: no score image) and the int16
+    score image + select path give the same bits: semantic, similar-sets with a mask (rank 0
+    masked or not), CF with rated exclusions and the hybrid blend, at B = 1, 37 and 256."""
+    rng = np.random.default_rng(21)
+    n, d, r, k = 25216, 384, 50, 50
+    x = R.unit_rows(n, d, 5)
+    x[[10, 20000]] = x[7000]          # exact duplicates of a liked set
+    f = rng.normal(0, 0.1, (n, r)).astype(np.float32)
+    mask = rng.random(n) < 0.3
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(x)
+    idx.upload_cf(f)
+    for B in (1, 37, 256):
+        q = rng.standard_normal((B, d)).astype(np.float32)
+        qi = rng.choice(n, B, replace=False)
+        qi[0] = 7000
+        u = rng.normal(0, 0.1, (B, r)).astype(np.float32)
+        excl = rng.random((B, n)) < 0.01
+        runs = {}
+        for opt in (1, 0):
+            idx.set_option("rr_lists", opt)
+            runs[opt] = [idx.search("semantic", k, q_rows=q),
+                         idx.search("similar", k, q_items=qi, mask=mask),
+                         idx.search("similar", 10, q_items=qi),
+                         idx.search("cf", k, q_cf=u, excl=excl, mask=mask),
+                         idx.search("hybrid", k, q_items=qi, q_cf=u, excl=excl, mask=mask)]
+        idx.set_option("rr_lists", -1)
+        for j, (a, b) in enumerate(zip(runs[1], runs[0])):
+            for t in range(3):
+                assert np.array_equal(a[t], b[t]), (B, j, t)
