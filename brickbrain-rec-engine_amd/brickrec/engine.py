@@ -98,23 +98,29 @@ class ItemIndex:
         v = ItemIndex.__new__(ItemIndex)
         v._lib, v.dtype, v.device, v.id_offset = self._lib, self.dtype, self.device, self.id_offset
         h = C.c_void_p()
-        with self._mu:
+        with self._mu:  # the view count changes under the base's lock (view(), close())
             L.check(self._lib.bb_create_view(self._h, C.byref(h)), "bb_create_view")
+            self._views = getattr(self, "_views", 0) + 1
         v._h = h
         v._mu = threading.Lock()
         v.n_items, v.d, v.r = self.n_items, self.d, self.r
         v._base = self  # keeps the base alive while the view is
-        self._views = getattr(self, "_views", 0) + 1
         return v
 
     def close(self):
-        if getattr(self, "_h", None):
-            base = getattr(self, "_base", None)
+        mu = getattr(self, "_mu", None)
+        if mu is None:
+            return
+        with mu:
+            if not getattr(self, "_h", None):
+                return
             if getattr(self, "_views", 0):
                 raise L.BrickrecError("close this index's views first")
             L.check(self._lib.bb_destroy(self._h), "bb_destroy")
             self._h = None
-            if base is not None:
+        base = getattr(self, "_base", None)
+        if base is not None:
+            with base._mu:
                 base._views -= 1
 
     def __del__(self):
@@ -359,31 +365,41 @@ class ItemIndex:
                             w_content: float = 0.4, w_cf: float = 0.6):
         """HYBRID in one device pass with each final item's side membership: bb_search (both
         sides scored and selected in the same search, key lists out) then bb_finalize (rank-0
-        drop, union blend wc·c + wcf·cf in f64 on the device).  Host inputs; returns numpy
-        (scores [B,k], ids [B,k], counts [B], in_content [B,k] bool, in_cf [B,k] bool, side
-        lists [B] of (content ids, CF ids)).  The membership is what
+        drop, union blend wc·c + wcf·cf in f64 on the device).  Host numpy in and out through
+        ctypes (no torch): returns (scores [B,k], ids [B,k], counts [B], in_content [B,k] bool,
+        in_cf [B,k] bool, side lists [B] of (content ids, CF ids)).  The membership is what
         _combine_recommendations (recommendation_system.py:789-843) builds its reasons from."""
-        import torch
-        dev = torch.device("cuda", self.device)
-        qi = torch.as_tensor(np.ascontiguousarray(np.asarray(q_items, np.int64))).to(dev)
-        qc_np = np.ascontiguousarray(q_cf if np.asarray(q_cf).dtype in (np.float32, np.float64)
-                                     else np.asarray(q_cf, np.float64))
-        qc = torch.as_tensor(qc_np).to(dev)
-        words = lambda m: None if m is None else torch.as_tensor(
-            (np.asarray(m, np.uint32) if np.asarray(m).dtype == np.uint32 else bits_from_bool(m)).view(np.int32)).to(dev)
-        keys, maxk = self.search_keys("hybrid", k, q_items=qi, q_cf=qc, mask=words(mask), excl=words(excl),
-                                      k_side=k_side)
-        sc, ids, cnt = self.finalize("hybrid", k, keys[None], maxk[None], 1, k_side=k_side, w_content=w_content,
-                                     w_cf=w_cf)
-        sc, ids, cnt = sc.cpu().numpy(), ids.cpu().numpy(), cnt.cpu().numpy()
-        kk = keys.cpu().numpy().view(np.uint64)
-        mk = maxk.cpu().numpy().view(np.uint64)
+        qi = np.ascontiguousarray(np.asarray(q_items, np.int64))
+        B = int(qi.shape[0])
+        qc = np.ascontiguousarray(q_cf if np.asarray(q_cf).dtype in (np.float32, np.float64)
+                                  else np.asarray(q_cf, np.float64))
+        words = lambda m: None if m is None else np.ascontiguousarray(
+            np.asarray(m, np.uint32) if np.asarray(m).dtype == np.uint32 else bits_from_bool(m))
+        mw, ew = words(mask), words(excl)
+        sides_n, kint = self.key_lens("hybrid", k, k_side)
+        keys = np.zeros((1, sides_n, B, kint), np.uint64)
+        maxk = np.zeros((1, B), np.uint64)
+        ptr = lambda a: None if a is None else a.ctypes.data
+        q = self._query("hybrid", k, B, k_side, L.BB_HOST, None, 0, qi.ctypes.data, qc.ctypes.data,
+                        _np_dtype_code(qc), ptr(mw), ptr(ew), w_content, w_cf, None, L.BB_Q_OUT_KEYS)
+        res = L.bb_result(None, None, None, L.BB_HOST, keys.ctypes.data, maxk.ctypes.data)
+        sc = np.zeros((B, k), np.float32)
+        ids = np.zeros((B, k), np.int64)
+        cnt = np.zeros(B, np.int32)
+        qf = self._query("hybrid", k, B, k_side, L.BB_HOST, None, 0, None, None, 0, None, None,
+                         w_content, w_cf, None, 0)
+        resf = L.bb_result(sc.ctypes.data, ids.ctypes.data, cnt.ctypes.data, L.BB_HOST, None, None)
+        with self._mu:
+            L.check(self._lib.bb_search(self._h, C.byref(q), C.byref(res)), "bb_search(keys)")
+            L.check(self._lib.bb_finalize(self._h, C.byref(qf), keys.ctypes.data, maxk.ctypes.data, 1,
+                                          C.byref(resf)), "bb_finalize")
+        kk, mk = keys[0], maxk[0]
         ks = k_side or 2 * k
         gid = lambda u: (np.uint64(0xFFFFFFFF) - (u & np.uint64(0xFFFFFFFF))).astype(np.int64)
         in_c = np.zeros(ids.shape, bool)
         in_f = np.zeros(ids.shape, bool)
         sides = []
-        for b in range(ids.shape[0]):
+        for b in range(B):
             c = kk[0, b][kk[0, b] != 0]
             if len(c) and mk[b] and c[0] == mk[b]:   # the rank-0 drop finalize applies
                 c = c[1:]

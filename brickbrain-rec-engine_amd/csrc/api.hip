@@ -158,6 +158,26 @@ int leave_stream(bb_index* x, hipStream_t s) {
   x->has_last = true;
   return BB_OK;
 }
+// Entered stream of one call: leave() on success; on an early error return the destructor
+// still records `done` on s, so work already queued there is covered and a later call on
+// another stream waits for it.
+struct StreamScope {
+  bb_index* x = nullptr;
+  hipStream_t s = nullptr;
+  int enter(bb_index* xi, hipStream_t si) {
+    const int rc = enter_stream(xi, si);
+    if (rc == BB_OK) x = xi, s = si;
+    return rc;
+  }
+  int leave() {
+    bb_index* xi = x;
+    x = nullptr;
+    return xi ? leave_stream(xi, s) : BB_OK;
+  }
+  ~StreamScope() {
+    if (x) (void)leave_stream(x, s);
+  }
+};
 
 // Run a launcher with optional event bracketing for the profiler.
 template <typename F>
@@ -309,11 +329,22 @@ int bb_create_view(bb_index* b, bb_index** out) {
 
 int bb_destroy(bb_index* x) {
   if (!x) return BB_OK;
-  if (x->n_views > 0) return fail(BB_E_STATE, "bb_destroy: destroy the index's views first");
-  if (x->base) --x->base->n_views;
+  {
+    std::lock_guard<std::mutex> lk(x->mu);  // bb_create_view counts views under it
+    if (x->n_views > 0) return fail(BB_E_STATE, "bb_destroy: destroy the index's views first");
+  }
   {
     DeviceGuard g(x->device);
+    // a view's kernels read its base's rows: they finish before the base may be destroyed
     (void)hipStreamSynchronize(x->stream);
+    if (x->has_last) (void)hipEventSynchronize(x->done);
+  }
+  if (x->base) {
+    std::lock_guard<std::mutex> lk(x->base->mu);
+    --x->base->n_views;
+  }
+  {
+    DeviceGuard g(x->device);
     for (auto& p : x->pending) {
       (void)hipEventDestroy(p.a);
       (void)hipEventDestroy(p.b);
@@ -350,7 +381,8 @@ int bb_get_rows(bb_index* x, const int64_t* ids, int32_t B, void* out, int32_t w
   const size_t es = elem_size(x->dtype);
   const int bpad = (int)round_up(B, kTileRows);
   int rc;
-  if ((rc = enter_stream(x, x->stream))) return rc;
+  StreamScope scope;
+  if ((rc = scope.enter(x, x->stream))) return rc;
   if ((rc = x->tmp.ensure((size_t)bpad * x->Dpad * es + (size_t)B * 8 + 256))) return rc;
   char* rows = (char*)x->tmp.p;
   const int64_t* d_ids = ids;
@@ -374,7 +406,7 @@ int bb_get_rows(bb_index* x, const int64_t* ids, int32_t B, void* out, int32_t w
   BB_HIP(hipMemcpy2DAsync(out, (size_t)x->d * es, rows, (size_t)x->Dpad * es, (size_t)x->d * es, B,
                           where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, x->stream));
   BB_HIP(hipStreamSynchronize(x->stream));
-  return leave_stream(x, x->stream);
+  return scope.leave();
 }
 
 // Upload rows (host or device) in chunks through the staging buffer and convert them into
@@ -439,13 +471,14 @@ static int make_rr(bb_index* x, DevBuf& rows, DevBuf& bf, int ld, int& ld_b, int
 int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t in_dtype, int32_t prenormalized,
                     int32_t where, const uint32_t* present_bits) {
   if (x && x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
-  if (x && x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
   if (!x || !rows || n <= 0 || d <= 0) return fail(BB_E_ARG, "bb_upload_items: bad arguments");
   if (in_dtype != F32 && in_dtype != BF16 && in_dtype != F64) return fail(BB_E_ARG, "bad input dtype");
   if (n >= 0xFFFFFFFFll - x->id_offset) return fail(BB_E_ARG, "too many items for 32-bit ids");
-  std::lock_guard<std::mutex> lk(x->mu);
+  std::lock_guard<std::mutex> lk(x->mu);  // bb_create_view takes it too
+  if (x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
   DeviceGuard g(x->device);
-  if (int rc0 = enter_stream(x, x->stream)) return rc0;
+  StreamScope scope;
+  if (int rc0 = scope.enter(x, x->stream)) return rc0;
   x->n = n;
   x->d = d;
   x->Npad = round_up(n, kTileRows);
@@ -469,17 +502,18 @@ int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t
   if ((rc = upload_rows(x, rows, n, d, in_dtype, prenormalized ? 0 : 1, where, x->items.p, x->Dpad))) return rc;
   if ((rc = make_planes(x, x->items, x->items3, x->Dpad))) return rc;
   if ((rc = make_rr(x, x->items, x->items_bf, x->Dpad, x->Dpad_b, 0))) return rc;
-  return leave_stream(x, x->stream);
+  return scope.leave();
 }
 
 int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const uint32_t* present_bits) {
   if (x && x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
-  if (x && x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
   if (!x || !f || r <= 0) return fail(BB_E_ARG, "bb_upload_cf: bad arguments");
   if (x->n <= 0) return fail(BB_E_STATE, "upload items before CF factors");
-  std::lock_guard<std::mutex> lk(x->mu);
+  std::lock_guard<std::mutex> lk(x->mu);  // bb_create_view takes it too
+  if (x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
   DeviceGuard g(x->device);
-  if (int rc0 = enter_stream(x, x->stream)) return rc0;
+  StreamScope scope;
+  if (int rc0 = scope.enter(x, x->stream)) return rc0;
   x->r = r;
   x->Rpad = (int)round_up(r, gemm_tile_k(x->dtype));
   const size_t bytes = (size_t)x->Npad * x->Rpad * elem_size(x->dtype);
@@ -498,25 +532,26 @@ int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const 
   if ((rc = upload_rows(x, f, x->n, r, in_dtype, 0, BB_HOST, x->cf.p, x->Rpad))) return rc;
   if ((rc = make_planes(x, x->cf, x->cf3, x->Rpad))) return rc;
   if ((rc = make_rr(x, x->cf, x->cf_bf, x->Rpad, x->Rpad_b, 4))) return rc;
-  return leave_stream(x, x->stream);
+  return scope.leave();
 }
 
 int bb_upload_attrs(bb_index* x, const int32_t* num_parts, const int16_t* year, const int32_t* theme_id) {
   if (x && x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
-  if (x && x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
   if (!x || !num_parts || !year || !theme_id) return fail(BB_E_ARG, "bb_upload_attrs: bad arguments");
   if (x->n <= 0) return fail(BB_E_STATE, "upload items before attributes");
-  std::lock_guard<std::mutex> lk(x->mu);
+  std::lock_guard<std::mutex> lk(x->mu);  // bb_create_view takes it too
+  if (x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
   DeviceGuard g(x->device);
   int rc;
-  if ((rc = enter_stream(x, x->stream))) return rc;
+  StreamScope scope;
+  if ((rc = scope.enter(x, x->stream))) return rc;
   if ((rc = x->parts.ensure(x->n * 4)) || (rc = x->year.ensure(x->n * 2)) || (rc = x->theme.ensure(x->n * 4)))
     return rc;
   BB_HIP(hipMemcpyAsync(x->parts.p, num_parts, x->n * 4, hipMemcpyHostToDevice, x->stream));
   BB_HIP(hipMemcpyAsync(x->year.p, year, x->n * 2, hipMemcpyHostToDevice, x->stream));
   BB_HIP(hipMemcpyAsync(x->theme.p, theme_id, x->n * 4, hipMemcpyHostToDevice, x->stream));
   BB_HIP(hipStreamSynchronize(x->stream));
-  return leave_stream(x, x->stream);
+  return scope.leave();
 }
 
 int bb_eval_mask(bb_index* x, const bb_predicate* p, uint32_t* out_bits, int32_t where) {
@@ -527,7 +562,8 @@ int bb_eval_mask(bb_index* x, const bb_predicate* p, uint32_t* out_bits, int32_t
   const int64_t nw = (x->n + 31) / 32;
   const size_t tb = (size_t)((std::max(p->n_theme_bits, 0) + 31) / 32) * 4;
   const size_t ib = (size_t)std::max<int64_t>(p->n_excluded, 0) * 8;
-  int rc = enter_stream(x, x->stream);
+  StreamScope scope;
+  int rc = scope.enter(x, x->stream);
   if (rc) return rc;
   if ((rc = x->stage_in.ensure(nw * 4 + tb + ib + 64))) return rc;
   char* base = (char*)x->stage_in.p;
@@ -561,7 +597,7 @@ int bb_eval_mask(bb_index* x, const bb_predicate* p, uint32_t* out_bits, int32_t
     BB_HIP(hipMemcpyAsync(out_bits, dout, nw * 4, hipMemcpyDeviceToHost, x->stream));
   }
   BB_HIP(hipStreamSynchronize(x->stream));
-  return leave_stream(x, x->stream);
+  return scope.leave();
 }
 
 int bb_key_lens(const bb_query* q, int32_t* sides, int32_t* k_int) { return side_k_int(q, sides, k_int); }
@@ -1105,8 +1141,58 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
             continue;
           }
           const bool both = q->mode == BB_MODE_HYBRID && side == 1 && list_c;
+          static const bool ls_trace = getenv("BB_SELECT_TRACE") != nullptr;
+          if (ls_trace) {  // probe runs: phase stamps of side 0's rows (16 words per row)
+            if ((rc = x->trace.ensure((size_t)bc * 16 * 8))) return rc;
+            BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 128, s));
+            (both ? sa_dual0 : sa).trace = (uint64_t*)x->trace.p;
+          }
           if ((rc = timed(x, K_SELECT, s, [&] { return launch_select_list(both ? sa_dual0 : sa, both ? &sa : nullptr, bc, s); })))
             return rc;
+          if (ls_trace) {
+            std::vector<uint64_t> tr((size_t)bc * 16);
+            BB_HIP(hipMemcpyAsync(tr.data(), x->trace.p, tr.size() * 8, hipMemcpyDeviceToHost, s));
+            BB_HIP(hipStreamSynchronize(s));
+            double acc[8] = {0}, oacc[8] = {0}, nc = 0, ov_items = 0, r0_items = 0, st_max = 0, st_avg = 0;
+            int rows = 0, ovf_rows = 0, fb_rows = 0;
+            uint64_t t0 = ~0ull, t1 = 0;
+            for (int i = 0; i < bc; ++i) t0 = std::min<uint64_t>(t0, tr[(size_t)i * 16] ? tr[(size_t)i * 16] : ~0ull);
+            for (int i = 0; i < bc; ++i) {
+              const uint64_t* t = &tr[(size_t)i * 16];
+              if (t[10]) { ++fb_rows; continue; }
+              if (!t[7]) continue;
+              const bool ov = (t[8] >> 32) != 0;
+              ++rows;
+              ovf_rows += ov;
+              for (int j = 1; j < 8; ++j) (ov ? oacc : acc)[j] += t[j] ? (double)(t[j] - t[0]) : 0.0;
+              nc += (double)(uint32_t)t[8];
+              ov_items += (double)(uint32_t)t[9];
+              r0_items += (double)(t[9] >> 32);
+              st_max = std::max(st_max, (double)(t[0] - t0));
+              st_avg += (double)(t[0] - t0);
+              t1 = std::max(t1, t[7]);
+            }
+            const int nr = std::max(rows - ovf_rows, 1), no = std::max(ovf_rows, 1), ra = std::max(rows, 1);
+            fprintf(stderr, "[bb list select trace] rows=%d (overflowed %d, fallback %d) us-from-row-start: loaded %.2f "
+                    "bound %.2f classified %.2f appended %.2f rescored %.2f gmax %.2f end %.2f | overflow rows: "
+                    "appended %.2f rescored %.2f end %.2f | cands %.1f ovf items %.1f r0 items %.1f | row start "
+                    "avg %.2f max %.2f  span %.2f us\n", rows, ovf_rows, fb_rows, acc[1] / nr / 100, acc[2] / nr / 100,
+                    acc[3] / nr / 100, acc[4] / nr / 100, acc[5] / nr / 100, acc[6] / nr / 100, acc[7] / nr / 100,
+                    oacc[4] / no / 100, oacc[5] / no / 100, oacc[7] / no / 100, nc / ra, ov_items / ra, r0_items / ra,
+                    st_avg / ra / 100, st_max / 100, (double)(t1 - t0) / 100);
+            std::vector<int> ord(bc);
+            for (int i = 0; i < bc; ++i) ord[i] = i;
+            std::sort(ord.begin(), ord.end(), [&](int u, int w) { return tr[(size_t)u * 16 + 7] > tr[(size_t)w * 16 + 7]; });
+            for (int k = 0; k < std::min(bc, 4); ++k) {  // the slowest rows
+              const uint64_t* t = &tr[(size_t)ord[k] * 16];
+              if (!t[7]) break;
+              fprintf(stderr, "   slow row %d: start %.2f end %.2f | loaded %.2f bound %.2f cls %.2f app %.2f resc %.2f "
+                      "| cands %u lists-ovf %u ovf items %u r0 items %u\n", ord[k], (double)(t[0] - t0) / 100,
+                      (double)(t[7] - t0) / 100, (double)(t[1] - t[0]) / 100, (double)(t[2] - t[0]) / 100,
+                      (double)(t[3] - t[0]) / 100, (double)(t[4] - t[0]) / 100, (double)(t[5] - t[0]) / 100,
+                      (uint32_t)t[8], (uint32_t)(t[8] >> 32), (uint32_t)t[9], (uint32_t)(t[9] >> 32));
+            }
+          }
           continue;
         }
         // BB_SELECT_TRACE (probe runs): per-phase s_memrealtime stamps of every query row,
@@ -1197,14 +1283,17 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     }
     if (fuse_final) continue;
     const uint64_t* fin_keys = keys + (size_t)final_pp * sides * side_keys;
-    if (out_keys) {
+    if (out_keys) {  // key lists out: device buffers, or host buffers (copied, synchronised below)
+      const hipMemcpyKind kind = res->where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
       for (int side = 0; side < sides; ++side)
         BB_HIP(hipMemcpyAsync(res->keys + ((size_t)side * B + b0) * K_int, fin_keys + (size_t)side * side_keys,
-                              (size_t)bc * K_int * 8, hipMemcpyDeviceToDevice, s));
+                              (size_t)bc * K_int * 8, kind, s));
       if (drop)
-        BB_HIP(hipMemcpyAsync(res->max_keys + b0, maxk, (size_t)bc * 8, hipMemcpyDeviceToDevice, s));
-      else
+        BB_HIP(hipMemcpyAsync(res->max_keys + b0, maxk, (size_t)bc * 8, kind, s));
+      else if (res->where == BB_DEVICE)
         BB_HIP(hipMemsetAsync(res->max_keys + b0, 0, (size_t)bc * 8, s));
+      else
+        memset(res->max_keys + b0, 0, (size_t)bc * 8);
       continue;
     }
     FinalizeArgs fa{};
@@ -1287,7 +1376,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     BB_HIP(hipMemcpyAsync(res->ids, o_id, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
     if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, o_cnt, (size_t)B * 4, hipMemcpyDeviceToHost, s));
   }
-  if (host_out || where == BB_HOST) BB_HIP(hipStreamSynchronize(s));
+  if (host_out || where == BB_HOST || (out_keys && res->where != BB_DEVICE)) BB_HIP(hipStreamSynchronize(s));
   return BB_OK;
 }
 
@@ -1322,7 +1411,8 @@ int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
   const hipStream_t s = call_stream(x, q);
-  if ((rc = enter_stream(x, s))) return rc;
+  StreamScope scope;
+  if ((rc = scope.enter(x, s))) return rc;
   const int B = q->B;
   const bool host_out = res->where != BB_DEVICE;
   if (host_out) {
@@ -1331,6 +1421,14 @@ int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint
       return rc;
   }
   const bool drop = q->mode == BB_MODE_SIMILAR || q->mode == BB_MODE_HYBRID;
+  if (q->where != BB_DEVICE) {  // host key lists (q->where): staged to the device
+    const size_t kb = (size_t)n_parts * sides * B * K_int * 8, mb = drop ? (size_t)n_parts * B * 8 : 0;
+    if ((rc = x->stage_in.ensure(kb + mb + 64))) return rc;
+    BB_HIP(hipMemcpyAsync(x->stage_in.p, keys, kb, hipMemcpyHostToDevice, s));
+    if (mb) BB_HIP(hipMemcpyAsync((char*)x->stage_in.p + kb, max_keys, mb, hipMemcpyHostToDevice, s));
+    keys = (const uint64_t*)x->stage_in.p;
+    max_keys = mb ? (const uint64_t*)((char*)x->stage_in.p + kb) : nullptr;
+  }
   FinalizeArgs fa{};
   fa.keys = keys;
   fa.max_keys = drop ? max_keys : nullptr;
@@ -1355,7 +1453,7 @@ int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint
     if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, x->out_cnt.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
     BB_HIP(hipStreamSynchronize(s));
   }
-  return leave_stream(x, s);
+  return scope.leave();
 }
 
 int bb_set_option(bb_index* x, int32_t option, int64_t value) {

@@ -118,8 +118,10 @@ __device__ __forceinline__ uint32_t list_r0_key(float m, float k2, uint32_t toff
 // Tiles of item chunk c (the scans' balanced split) and list geometry shared by host and
 // device: lists of chunk c, period p, lane (h, r) of 32-query block b at
 // ((c·np + p)·NB + b)·64 + h·32 + r (uint4); rank-0 pairs at (c·NB + b)·64 + h·32 + r (uint2).
+// (32-bit: the list geometry keeps chunks <= 256 and tiles < 2^24, so c·tiles < 2^32; the
+// scans' 64-bit split gives the same value)
 __host__ __device__ inline int chunk_tile_lo(int c, int tiles, int n_chunks) {
-  return (int)((int64_t)c * tiles / n_chunks);
+  return (int)((uint32_t)c * (uint32_t)tiles / (uint32_t)n_chunks);
 }
 __host__ __device__ inline size_t list_slot(int c, int p, int np, int nb, int b, int lane) {
   return (((size_t)c * np + p) * nb + b) * 64 + lane;

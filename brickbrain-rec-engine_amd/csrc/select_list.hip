@@ -6,51 +6,57 @@
 // ORDER BY <=> LIMIT k — for the 25K-row configs.  One workgroup (4 waves) per query row:
 //
 //   lists   every lane's top-4 keys per period (list_epi.h): key = (u16 code, chunk position)
-//   bound   T0 = the K-th largest list head: K distinct items have codes >= T0, so the exact
-//           K-th score is >= dec(T0) − ε', and every exact top-K member has code >= Tg =
-//           T0 − Δ (Δ = the re-rank margin 2ε'(1+2^-10)+2^-20 in codes, + 2 codes of slack)
+//   bound   T0 = the K-th largest code over ALL list keys (two-level histogram): K distinct
+//           items have codes >= T0, so the exact K-th score is >= dec(T0) − ε', and every
+//           exact top-K member has code >= Tg = T0 − Δ (Δ = the re-rank margin
+//           2ε'(1+2^-10)+2^-20 in codes, + 2 codes of slack)
 //   gather  keys >= Tg of the lists whose 4th key is below Tg (they dropped nothing that
-//           matters); lists whose 4th key reaches Tg may have dropped candidates, so all
-//           eligible items of their period are enumerated instead ("segments")
-//   rank 0  (similar / hybrid content side) the present half tiles whose maximum is within
-//           Δ of the largest; a lane whose 2nd-best half tile is also within Δ contributes its
-//           whole chunk half.  Their present items are rescored exactly; the exact maximum is
-//           the unmasked arg-max key that the similar-sets path drops (:217)
-//   rescore every candidate from the f32 rows (f64 sums in rescore_rows' fixed order, rounded
-//           to f32: the same bits as every other path), sort by (score desc, id asc), emit
-// Common case (no segments, <= 512 candidates): one rescore round + a register sort by one
-// wave.  Otherwise an exact running top-K: candidates and enumerated items are rescored in
-// batches and merged by a bitonic sort in LDS (masses of near-duplicates, all-equal scores).
+//           matters); a list whose 4th key reaches Tg may have dropped candidates, so every
+//           eligible item of its period joins the buffer instead (an overflowed list: a few
+//           rows per batch at configs[1])
+//   rank 0  (similar / hybrid content side) the present half tiles whose maximum is within Δ
+//           of the largest; a lane whose 2nd-best half tile is also within Δ contributes its
+//           whole chunk half.  Their present items join the same buffer (a region of their
+//           own); the exact maximum among them is the unmasked arg-max key that the
+//           similar-sets path drops (:217)
+//   rescore the whole buffer in ONE pass from the f32 rows (f64 sums in rescore_rows' fixed
+//           order, rounded to f32: the same bits as every other path), 64 rows in flight
+//   emit    sort the candidates by (score desc, id asc) — one wave in registers up to 512,
+//           an LDS bitonic network up to kLsCand — drop rank 0, write the list
+// Buffer overflow (masses of near-duplicates, all-equal scores): an exact running top-K over
+// every eligible item of the row (slow, never taken on distinct data; tests drive it).
 #include "common.h"
 #include "list_epi.h"
 #include "select_util.h"
 
 namespace bb {
 
-constexpr int kLsCand = 2048;   // candidate / batch buffer (u64 keys)
-constexpr int kLsFlush = 1024;  // batch size that triggers a merge of the running top-K
-constexpr int kLsSeg = 512;     // content segments (overflowing lists)
+constexpr int kLsCand = 2048;   // rescore buffer (u64 keys): candidates + overflow items + rank-0 items
+constexpr int kLsFlush = 1024;  // fallback: batch size that triggers a merge of the running top-K
+constexpr int kLsSeg = 64;      // overflowed lists
 constexpr int kLsR0Seg = 64;    // rank-0 segments
 constexpr int kLsMaxLists = 1024;
 constexpr int kLsOffCand = 0;
-constexpr int kLsOffSel = kLsOffCand + kLsCand * 8;          // u64 [kMaxKInt] running top-K
-constexpr int kLsOffHd = kLsOffSel + kMaxKInt * 8;           // u32 [kLsMaxLists] head codes
-constexpr int kLsOffSeg = kLsOffHd + kLsMaxLists * 4;        // u32 [kLsSeg][2] (t0, nt << 1 | h)
-constexpr int kLsOffPre = kLsOffSeg + kLsSeg * 8;            // u32 [kLsSeg + 1] item prefix
-constexpr int kLsOffR0 = kLsOffPre + (kLsSeg + 1) * 4 + 12;  // u32 [kLsR0Seg][2]
+constexpr int kLsOffSel = kLsOffCand + kLsCand * 8;          // u64 [kMaxKInt] running top-K (fallback)
+constexpr int kLsOffHist = kLsOffSel + kMaxKInt * 8;         // u32 [256] bound histogram
+constexpr int kLsOffSeg = kLsOffHist + 256 * 4;              // u32 [kLsSeg][2] (t0, nt << 1 | h)
+constexpr int kLsOffR0 = kLsOffSeg + kLsSeg * 8;             // u32 [kLsR0Seg][2]
 constexpr int kLsOffQs = kLsOffR0 + kLsR0Seg * 8;            // f32 [kRrMaxD]
 constexpr int kLsOffMisc = kLsOffQs + kRrMaxD * 4;           // u32 [16]
-constexpr int kLsOffAll = kLsOffMisc + 64;                   // u32 [4] + [3]: every item of the row
+constexpr int kLsOffScan = kLsOffMisc + 64;                  // u32 [8]: block scan / find_bin words
+constexpr int kLsOffAll = kLsOffScan + 32;                   // u32 [4] + [3]: every item of the row
 constexpr int kLsLds = kLsOffAll + 32;
 static_assert(kLsOffQs % 16 == 0, "query row must be 16-B aligned");
+static_assert(kSelectThreads == 256, "one histogram bin per thread");
 // misc words; M_GMAX is a u64 (8-byte aligned: misc starts 8-aligned)
-enum { M_CAND = 0, M_SEG, M_R0SEG, M_BUF, M_PM, M_GMAX = 8 };
+enum { M_CAND = 0, M_SEG, M_R0SEG, M_BUF, M_PM, M_SEGN, M_R0N, M_GMAX = 8 };
 static_assert(kLsOffMisc % 8 == 0, "u64 misc word must be 8-byte aligned");
 
-// Exhaustive enumeration of segments (tile ranges of one lane half) in rounds of 256 items:
+// Fallback enumeration of segments (tile ranges of one lane half) in rounds of 256 items:
 // item i of the concatenation -> (segment, tile, register) by binary search over the item
 // prefix; items passing `keep` are appended to buf as placeholder keys; a batch reaching
-// `flush` items is reduced (merge or max); at most flush - 1 + 256 items are buffered.  Every thread returns holding the same buffer count.
+// `flush` items is reduced (merge or max); at most flush - 1 + 256 items are buffered.  Every
+// thread returns holding the same buffer count.
 template <typename Keep, typename Reduce>
 __device__ __forceinline__ void ls_stream(const uint32_t* seg, const uint32_t* pre, int nseg, uint64_t* buf, uint32_t* misc,
                           uint32_t gid0, int n, int flush, Keep keep, Reduce reduce) {
@@ -77,16 +83,47 @@ __device__ __forceinline__ void ls_stream(const uint32_t* seg, const uint32_t* p
   }
 }
 
+// Append the items of segments seg[0..ns) (tile t0, nt tiles, lane half h) that pass `keep`
+// to buf at misc[M_CAND] (no capacity check beyond the buffer: the caller sized it).
+template <typename Keep>
+__device__ __forceinline__ void ls_append(const uint32_t* seg, int ns, uint64_t* buf, uint32_t* misc, uint32_t gid0, int n,
+                                          Keep keep) {
+  for (int s = 0; s < ns; ++s) {
+    const int t0 = (int)seg[2 * s], hh = (int)(seg[2 * s + 1] & 1u), cnt = (int)(seg[2 * s + 1] >> 1) * 16;
+    for (int i = threadIdx.x; i < cnt; i += kSelectThreads) {
+      const int tile = t0 + (i >> 4), g = i & 15;
+      const int it = (g & 3) + 8 * (g >> 2) + 4 * hh, j = tile * 32 + it;
+      if (j < n && keep(tile, it)) {
+        const uint32_t p = atomicAdd(&misc[M_CAND], 1u);
+        if (p < (uint32_t)kLsCand) buf[p] = make_key(1u, gid0 + (uint32_t)j);
+      }
+    }
+  }
+}
+
+// The rescore of the list select: one pass, as many rows in flight as the registers allow
+// (one select wave per SIMD; the scan of the next batch cannot share the CU anyway).
+__device__ __forceinline__ void ls_rescore(uint64_t* keys, int m, const SelectArgs& a, const float* qs) {
+  const int cpl = ((a.rr_d >> 2) + 15) >> 4;
+  const int t = threadIdx.x;
+  if (cpl <= 1) rescore_rows<1, 16, 16>(keys, m, a, qs, t);
+  else if (cpl <= 2) rescore_rows<2, 8, 16>(keys, m, a, qs, t);
+  else if (cpl <= 4) rescore_rows<4, 4, 16>(keys, m, a, qs, t);
+  else if (cpl <= 6) rescore_rows<6, 4, 16>(keys, m, a, qs, t);
+  else rescore_rows<8, 2, 16>(keys, m, a, qs, t);   // rows up to kRrMaxD = 512 wide
+}
+
 __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   __shared__ __attribute__((aligned(16))) char dsm[kLsLds];
   uint64_t* cand = (uint64_t*)(dsm + kLsOffCand);
   uint64_t* sel = (uint64_t*)(dsm + kLsOffSel);
-  uint32_t* hd = (uint32_t*)(dsm + kLsOffHd);
+  uint32_t* hist = (uint32_t*)(dsm + kLsOffHist);
   uint32_t* seg = (uint32_t*)(dsm + kLsOffSeg);
-  uint32_t* pre = (uint32_t*)(dsm + kLsOffPre);
   uint32_t* r0s = (uint32_t*)(dsm + kLsOffR0);
   float* qs = (float*)(dsm + kLsOffQs);
   uint32_t* misc = (uint32_t*)(dsm + kLsOffMisc);
+  uint32_t* scan_sh = (uint32_t*)(dsm + kLsOffScan);
+  uint32_t* fb = scan_sh + 4;                        // find_bin results
   uint32_t* allseg = (uint32_t*)(dsm + kLsOffAll);  // both halves of every tile
   uint32_t* allpre = allseg + 4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -95,8 +132,13 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   const int L = 2 * NC * NP;
   const int blk = row >> 5, r = row & 31;
   const bool want_r0 = a.max_inout != nullptr;
+  auto stamp = [&](int slot) {  // BB_SELECT_TRACE probe runs: phase timeline (100 MHz), 16 words per row
+    if (a.trace && tid == 0) a.trace[row * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   if (tid < 16) misc[tid] = 0u;
+  hist[tid] = 0u;  // kSelectThreads == 256 bins
   if (tid == 0) {
     allseg[0] = 0u;
     allseg[1] = (uint32_t)T << 1;
@@ -131,116 +173,146 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
       }
     }
   }
-#pragma unroll
-  for (int i = 0; i < kLPT; ++i) {
-    const int j = tid + i * kSelectThreads;
-    if (j < kLsMaxLists) hd[j] = v[i].x >> 16;
-  }
-  __syncthreads();
-
-  // ---- bound: T0 = K-th largest head code (every wave on its own, ballot counts) ----
-  uint32_t Tg = 1u;
-  {
-    uint32_t hv[kLsMaxLists / 64];
-#pragma unroll
-    for (int i = 0; i < kLsMaxLists / 64; ++i) hv[i] = lane + 64 * i < L ? hd[lane + 64 * i] : 0u;
-    auto cnt_ge = [&](uint32_t c) -> uint32_t {
-      uint32_t s = 0;
-#pragma unroll
-      for (int i = 0; i < kLsMaxLists / 64; ++i) s += (uint32_t)__popcll(__ballot(hv[i] >= c));
-      return s;
-    };
-    if (cnt_ge(1u) >= (uint32_t)K) {
-      uint32_t hi = 0, lo = 0xFFFFu;
-#pragma unroll
-      for (int i = 0; i < kLsMaxLists / 64; ++i) {
-        hi = max(hi, hv[i]);
-        lo = min(lo, hv[i] ? hv[i] : 0xFFFFu);
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
-        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
-      }
-      hi = __builtin_amdgcn_readfirstlane(hi);
-      lo = __builtin_amdgcn_readfirstlane(lo);
-      const uint32_t d = hi ^ lo;
-      const int top = d ? 31 - __builtin_clz(d) : -1;
-      uint32_t P = top < 0 ? hi : hi & ~((2u << top) - 1u);
-      for (int b = top; b >= 0; --b) {
-        const uint32_t c = P | (1u << b);
-        if (cnt_ge(c) >= (uint32_t)K) P = c;
-      }
-      Tg = P > delta ? P - delta : 1u;
-    }
-  }
-
-  // ---- classify: candidates of complete lists, segments for the overflowing ones ----
-#pragma unroll
-  for (int i = 0; i < kLPT; ++i) {
-    if (vt0[i] < 0 || v[i].x == 0u) continue;
-    const int j = tid + i * kSelectThreads, hh = j & 1;
-    const int c = (j >> 1) / NP, tlo = chunk_tile_lo(c, T, NC);
-    if ((v[i].w >> 16) >= Tg) {  // all four within the margin: the period may hold more
-      const uint32_t s = atomicAdd(&misc[M_SEG], 1u);
-      const int thi = chunk_tile_lo(c + 1, T, NC), nt = min(G, thi - vt0[i]);
-      if (s < (uint32_t)kLsSeg) {
-        seg[2 * s] = (uint32_t)vt0[i];
-        seg[2 * s + 1] = ((uint32_t)nt << 1) | (uint32_t)hh;
-      }
-      continue;
-    }
-    // keys are sorted: the ones at or above Tg form a prefix
-    const uint32_t m = (uint32_t)((v[i].x >> 16) >= Tg) + (uint32_t)((v[i].y >> 16) >= Tg) +
-                       (uint32_t)((v[i].z >> 16) >= Tg);
-    if (!m) continue;
-    const uint32_t p0 = atomicAdd(&misc[M_CAND], m);
-    const uint32_t gb = a.gid0 + (uint32_t)(tlo * 32);
-    if (p0 < (uint32_t)kLsCand) cand[p0] = make_key(1u, gb + (v[i].x & 0xFFFFu));
-    if (m > 1 && p0 + 1 < (uint32_t)kLsCand) cand[p0 + 1] = make_key(1u, gb + (v[i].y & 0xFFFFu));
-    if (m > 2 && p0 + 2 < (uint32_t)kLsCand) cand[p0 + 2] = make_key(1u, gb + (v[i].z & 0xFFFFu));
-  }
-
-  // ---- rank 0: present half tiles within Δ of the largest present maximum ----
-  constexpr int kRPT = 2;  // (chunk, half) entries per thread: 2·NC <= 512
+  constexpr int kRPT = 2;  // rank-0 (chunk, half) entries per thread: 2·NC <= 512
   uint2 rv[kRPT];
-  if (want_r0) {
-    uint32_t pm = 0;
+  uint32_t pm = 0;
 #pragma unroll
-    for (int i = 0; i < kRPT; ++i) {
-      const int e = tid + i * kSelectThreads, c = e >> 1, hh = e & 1;
-      rv[i] = make_uint2(0u, 0u);
-      if (c < NC && chunk_tile_lo(c + 1, T, NC) > chunk_tile_lo(c, T, NC))
-        rv[i] = *(const uint2*)(a.r0lists + 2 * list_slot(c, 0, 1, a.l_nb, blk, hh * 32 + r));
-      pm = max(pm, rv[i].x >> 16);
+  for (int i = 0; i < kRPT; ++i) {
+    const int e = tid + i * kSelectThreads, c = e >> 1, hh = e & 1;
+    rv[i] = make_uint2(0u, 0u);
+    if (want_r0 && c < NC && chunk_tile_lo(c + 1, T, NC) > chunk_tile_lo(c, T, NC))
+      rv[i] = *(const uint2*)(a.r0lists + 2 * list_slot(c, 0, 1, a.l_nb, blk, hh * 32 + r));
+    pm = max(pm, rv[i].x >> 16);
+  }
+  __syncthreads();  // hist and misc cleared
+  stamp(1);
+
+  // ---- bound: T0 = K-th largest code over every list key, by a bitwise search: each wave
+  // counts its lanes' keys >= c with ballots, the four wave counts meet in LDS (two
+  // alternating slots, one barrier per step); only the bits below the highest bit in which
+  // the largest and smallest codes differ are searched ----
+  const int nlw = (L - wave * 64 + kSelectThreads - 1) / kSelectThreads;  // lists of this wave's lanes (upper bound)
+  auto wave_count_ge = [&](uint32_t c) -> uint32_t {
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kLPT; ++i) {
+      if (i < nlw) {
+        cnt += (uint32_t)__popcll(__ballot((v[i].x >> 16) >= c));
+        cnt += (uint32_t)__popcll(__ballot((v[i].y >> 16) >= c));
+        cnt += (uint32_t)__popcll(__ballot((v[i].z >> 16) >= c));
+        cnt += (uint32_t)__popcll(__ballot((v[i].w >> 16) >= c));
+      }
     }
+    return cnt;
+  };
+  uint32_t* xch = hist;  // [2][4] count slots + [4] hi / [4] lo
+  {
+    uint32_t hi = 0, lo = 0xFFFFu;
+#pragma unroll
+    for (int i = 0; i < kLPT; ++i) {
+      hi = max(hi, v[i].x >> 16);  // keys are sorted within a list: x is the largest
+      const uint32_t w = v[i].w >> 16, z = v[i].z >> 16, y = v[i].y >> 16, xx = v[i].x >> 16;
+      const uint32_t mn = w ? w : z ? z : y ? y : xx;
+      lo = mn ? min(lo, mn) : lo;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+      lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+    }
+    const uint32_t c1 = wave_count_ge(1u);
+    if (lane == 0) {
+      xch[8 + wave] = hi;
+      xch[12 + wave] = lo;
+      xch[wave] = c1;
+    }
+  }
+  if (want_r0) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) pm = max(pm, (uint32_t)__shfl_xor((int)pm, o));
     if (lane == 0) atomicMax(&misc[M_PM], pm);
   }
   __syncthreads();
-  const uint32_t ncand0 = misc[M_CAND], nseg = misc[M_SEG];
-  // (the rank-0 phase buffers in the upper half of cand: more candidates -> enumerate all)
-  const bool full_scan = ncand0 > (uint32_t)(kLsCand / 2) || nseg > (uint32_t)kLsSeg;
-  if (want_r0) {
-    const uint32_t Pm = misc[M_PM];
-    const uint32_t thr0 = Pm > delta ? Pm - delta : 1u;
-    if (Pm) {
+  uint32_t Tg = 1u;
+  const uint32_t hi = max(max(xch[8], xch[9]), max(xch[10], xch[11]));
+  const uint32_t lo = min(min(xch[12], xch[13]), min(xch[14], xch[15]));
+  if (xch[0] + xch[1] + xch[2] + xch[3] >= (uint32_t)K) {
+    const uint32_t d = hi ^ lo;
+    const int top = d ? 31 - __builtin_clz(d) : -1;
+    uint32_t P = top < 0 ? hi : hi & ~((2u << top) - 1u);
+    for (int bit = top, st = 1; bit >= 0; --bit, ++st) {
+      const uint32_t c = P | (1u << bit);
+      const uint32_t wc = wave_count_ge(c);
+      uint32_t* slot = xch + 4 * (st & 1);
+      if (lane == 0) slot[wave] = wc;
+      __syncthreads();
+      if (slot[0] + slot[1] + slot[2] + slot[3] >= (uint32_t)K) P = c;
+    }
+    Tg = P > delta ? P - delta : 1u;
+  }
+  stamp(2);
+
+  // ---- classify: candidates of complete lists (one LDS atomic per wave and list slot),
+  // overflowed lists as segments ----
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
 #pragma unroll
-      for (int i = 0; i < kRPT; ++i) {
-        const int e = tid + i * kSelectThreads, c = e >> 1, hh = e & 1;
-        if (c >= NC || (rv[i].x >> 16) < thr0) continue;
-        const int tlo = chunk_tile_lo(c, T, NC), thi = chunk_tile_lo(c + 1, T, NC);
-        const bool whole = (rv[i].y >> 16) >= thr0;  // a 2nd half tile within Δ: the whole chunk half
-        const uint32_t s = atomicAdd(&misc[M_R0SEG], 1u);
-        if (s < (uint32_t)kLsR0Seg) {
-          r0s[2 * s] = whole ? (uint32_t)tlo : (uint32_t)(tlo + (rv[i].x & 0xFFFFu));
-          r0s[2 * s + 1] = ((uint32_t)(whole ? thi - tlo : 1) << 1) | (uint32_t)hh;
-        }
+  for (int i = 0; i < kLPT; ++i) {
+    if (i >= nlw) continue;  // wave-uniform
+    const bool live = vt0[i] >= 0 && v[i].x != 0u;
+    const int j = tid + i * kSelectThreads, hh = j & 1;
+    const int c = live ? (j >> 1) / NP : 0;
+    const int tlo = live ? chunk_tile_lo(c, T, NC) : 0;
+    const bool ovf = live && (v[i].w >> 16) >= Tg;  // all four within the margin: the period may hold more
+    if (ovf) {
+      const uint32_t sidx = atomicAdd(&misc[M_SEG], 1u);
+      const int thi = chunk_tile_lo(c + 1, T, NC), nt = min(G, thi - vt0[i]);
+      atomicAdd(&misc[M_SEGN], (uint32_t)nt * 16u);
+      if (sidx < (uint32_t)kLsSeg) {
+        seg[2 * sidx] = (uint32_t)vt0[i];
+        seg[2 * sidx + 1] = ((uint32_t)nt << 1) | (uint32_t)hh;
+      }
+    }
+    // keys are sorted: the ones at or above Tg form a prefix
+    const uint32_t m = live && !ovf ? (uint32_t)((v[i].x >> 16) >= Tg) + (uint32_t)((v[i].y >> 16) >= Tg) +
+                                          (uint32_t)((v[i].z >> 16) >= Tg)
+                                    : 0u;
+    const uint64_t b0 = __ballot(m & 1u), b1 = __ballot((m >> 1) & 1u);
+    const uint32_t tot = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1);
+    if (!tot) continue;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&misc[M_CAND], tot);
+    base = (uint32_t)__shfl((int)base, 0);
+    const uint32_t p0 = base + (uint32_t)__popcll(b0 & lt_mask) + 2u * (uint32_t)__popcll(b1 & lt_mask);
+    const uint32_t gb = a.gid0 + (uint32_t)(tlo * 32);
+    if (m > 0 && p0 < (uint32_t)kLsCand) cand[p0] = make_key(1u, gb + (v[i].x & 0xFFFFu));
+    if (m > 1 && p0 + 1 < (uint32_t)kLsCand) cand[p0 + 1] = make_key(1u, gb + (v[i].y & 0xFFFFu));
+    if (m > 2 && p0 + 2 < (uint32_t)kLsCand) cand[p0 + 2] = make_key(1u, gb + (v[i].z & 0xFFFFu));
+  }
+  // rank 0: present half tiles within Δ of the largest present maximum
+  if (want_r0) {
+    const uint32_t Pm = misc[M_PM];  // settled by the barriers of the bound
+    const uint32_t thr0 = Pm > delta ? Pm - delta : 1u;
+#pragma unroll
+    for (int i = 0; i < kRPT; ++i) {
+      const int e = tid + i * kSelectThreads, c = e >> 1, hh = e & 1;
+      if (!Pm || c >= NC || (rv[i].x >> 16) < thr0) continue;
+      const int tlo = chunk_tile_lo(c, T, NC), thi = chunk_tile_lo(c + 1, T, NC);
+      const bool whole = (rv[i].y >> 16) >= thr0;  // a 2nd half tile within Δ: the whole chunk half
+      const uint32_t s = atomicAdd(&misc[M_R0SEG], 1u);
+      const int nt = whole ? thi - tlo : 1;
+      atomicAdd(&misc[M_R0N], (uint32_t)nt * 16u);
+      if (s < (uint32_t)kLsR0Seg) {
+        r0s[2 * s] = whole ? (uint32_t)tlo : (uint32_t)(tlo + (rv[i].x & 0xFFFFu));
+        r0s[2 * s + 1] = ((uint32_t)nt << 1) | (uint32_t)hh;
       }
     }
   }
   __syncthreads();
+  const uint32_t ncand0 = misc[M_CAND], nseg = misc[M_SEG], nr0 = misc[M_R0SEG];
+  const bool full_scan = nseg > (uint32_t)kLsSeg || nr0 > (uint32_t)kLsR0Seg ||
+                         ncand0 + misc[M_SEGN] + misc[M_R0N] > (uint32_t)kLsCand;
+  stamp(3);
+
   const int64_t w0 = a.slab_start >> 5;
   const uint32_t* excl = a.excl ? a.excl + (size_t)row * a.excl_ld : nullptr;
   auto present_bit = [&](int tile, int it) -> bool {
@@ -252,23 +324,119 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     return (w >> it) & 1u;
   };
 
-  // ---- exact rank 0 (into misc[M_GMAX*]) ----
-  uint64_t gmax = 0;
-  if (want_r0) {
-    const uint32_t nr0 = misc[M_R0SEG];
-    const bool r0_all = nr0 > (uint32_t)kLsR0Seg;  // masses at the top: every present item
-    if (!r0_all && tid == 0) {
-      uint32_t acc = 0;
-      for (uint32_t s = 0; s < nr0; ++s) {
-        pre[s] = acc;
-        acc += (r0s[2 * s + 1] >> 1) * 16;
+  if (!full_scan) {
+    // ---- the one-pass path: [candidates | overflowed lists' eligible items | rank-0 items] ----
+    if (nseg) ls_append(seg, (int)nseg, cand, misc, a.gid0, n, elig_bit);
+    __syncthreads();
+    const int Mc = (int)misc[M_CAND];
+    if (nr0) ls_append(r0s, (int)nr0, cand, misc, a.gid0, n, present_bit);
+    __syncthreads();
+    const int M = (int)misc[M_CAND];
+    stamp(4);
+    ls_rescore(cand, M, a, qs);
+    __syncthreads();
+    stamp(5);
+    uint64_t gmax = 0;
+    if (want_r0) {
+      uint64_t best = 0;
+      for (int i = Mc + tid; i < M; i += kSelectThreads) best = cand[i] > best ? cand[i] : best;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(best, o);
+        best = y > best ? y : best;
       }
-      pre[nr0] = acc;
+      if (lane == 0) atomicMax((unsigned long long*)(misc + M_GMAX), (unsigned long long)best);
+      __syncthreads();
+      gmax = *(const uint64_t*)(misc + M_GMAX);
+      if (tid == 0) a.max_inout[row] = gmax;
+    }
+    stamp(6);
+    if (a.trace && tid == 0) {
+      a.trace[row * 16 + 8] = ncand0 | ((uint64_t)nseg << 32);
+      a.trace[row * 16 + 9] = (uint64_t)(Mc - (int)ncand0) | ((uint64_t)(M - Mc) << 32);
+    }
+    // ranks by counting: key i's position = #keys larger (keys are distinct: distinct ids);
+    // every thread ranks its keys against the whole buffer with broadcast LDS reads, 16 keys
+    // per step with the next 16 already in flight (LDS latency bounds this loop).  The
+    // buffer is zero-padded to a multiple of 16 first (the rank-0 items there are consumed).
+    const int Mc16 = (Mc + 15) & ~15;
+    __syncthreads();
+    if (tid < Mc16 - Mc) cand[Mc + tid] = 0ull;
+    constexpr int kRk = kLsCand / kSelectThreads;
+    uint64_t mk[kRk];
+    uint32_t rk[kRk];
+#pragma unroll
+    for (int e = 0; e < kRk; ++e) {
+      const int i = tid + e * kSelectThreads;
+      mk[e] = i < Mc ? cand[i] : 0ull;
+      rk[e] = 0;
     }
     __syncthreads();
-    const int nsg = r0_all ? 2 : (int)nr0;
-    // the rank-0 items go to the upper half of the candidate buffer (the lower half holds
-    // the content candidates of the complete lists)
+    const int ne = (Mc + kSelectThreads - 1) / kSelectThreads;  // uniform
+    const ulonglong2* c2 = (const ulonglong2*)cand;
+    auto rank_pass = [&](auto NE) __attribute__((always_inline)) {
+      constexpr int E = decltype(NE)::value;
+      ulonglong2 ya[8], yb[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) ya[jj] = c2[jj];
+      for (int k = 0; k < Mc16; k += 16) {
+        const int kn = k + 16 < Mc16 ? k + 16 : k;  // (the last step re-reads, harmlessly)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) yb[jj] = c2[(kn >> 1) + jj];
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) rk[e] += (ya[jj].x > mk[e] ? 1u : 0u) + (ya[jj].y > mk[e] ? 1u : 0u);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) ya[jj] = yb[jj];
+      }
+    };
+    if (ne <= 1) rank_pass(std::integral_constant<int, 1>{});
+    else if (ne <= 2) rank_pass(std::integral_constant<int, 2>{});
+    else if (ne <= 4) rank_pass(std::integral_constant<int, 4>{});
+    else rank_pass(std::integral_constant<int, kRk>{});
+    const int cnt = min(Mc, K);
+    if (a.out_scores) {
+      // rank 0 dropped when it heads the list (the head is the unmasked arg-max iff that item
+      // is eligible: gmax is then among the candidates)
+      if (tid == 0) misc[M_BUF] = 0u;
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < kRk; ++e)
+        if (e < ne && tid + e * kSelectThreads < Mc && rk[e] == 0 && gmax && mk[e] == gmax) misc[M_BUF] = 1u;
+      __syncthreads();
+      const int start = (int)misc[M_BUF];
+      const int c = min(a.k_final, cnt - start);
+      float* sc = a.out_scores + (size_t)row * a.k_final;
+      int64_t* id = a.out_ids + (size_t)row * a.k_final;
+#pragma unroll
+      for (int e = 0; e < kRk; ++e) {
+        const int pos = (int)rk[e] - start;
+        if (e < ne && tid + e * kSelectThreads < Mc && pos >= 0 && pos < c) {
+          sc[pos] = float_of_ord(ordk_of(mk[e]));
+          id[pos] = (int64_t)gid_of(mk[e]);
+        }
+      }
+      for (int i = c + tid; i < a.k_final; i += kSelectThreads) {
+        sc[i] = 0.f;
+        id[i] = -1;
+      }
+      if (a.out_counts && tid == 0) a.out_counts[row] = c;
+    } else {
+      uint64_t* out = a.keys_out + (size_t)row * K;
+#pragma unroll
+      for (int e = 0; e < kRk; ++e)
+        if (e < ne && tid + e * kSelectThreads < Mc && rk[e] < (uint32_t)K) out[rk[e]] = mk[e];
+      for (int i = cnt + tid; i < K; i += kSelectThreads) out[i] = 0ull;
+    }
+    stamp(7);
+    return;
+  }
+
+  // ---- fallback: exact rank 0 over every present item, exact running top-K over every
+  // eligible item (masses of near-ties overflowing the buffer) ----
+  uint64_t gmax = 0;
+  if (want_r0) {
     uint64_t* rb = cand + kLsCand / 2;
     if (tid == 0) misc[M_BUF] = 0u;
     __syncthreads();
@@ -281,8 +449,7 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
       if (tid == 0) misc[M_BUF] = 0u;
       __syncthreads();
     };
-    // flush at 512: at most 767 < kLsCand / 2 items are buffered at once
-    ls_stream(r0_all ? allseg : r0s, r0_all ? allpre : pre, nsg, rb, misc, a.gid0, n, 512, present_bit, r0_reduce);
+    ls_stream(allseg, allpre, 2, rb, misc, a.gid0, n, 512, present_bit, r0_reduce);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const uint64_t y = __shfl_xor(best, o);
@@ -294,21 +461,8 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     if (tid == 0) a.max_inout[row] = gmax;
     __syncthreads();
   }
-
-  // ---- common case: every list complete, few candidates: one rescore, one register sort ----
-  if (!full_scan && nseg == 0 && ncand0 <= 512u) {
-    rr_rescore_any(cand, (int)ncand0, a, qs);
-    __syncthreads();
-    if (wave != 0) return;
-    if (ncand0 <= 64) wave_sort_emit<1>(cand, (int)ncand0, a, row, gmax);
-    else if (ncand0 <= 128) wave_sort_emit<2>(cand, (int)ncand0, a, row, gmax);
-    else if (ncand0 <= 256) wave_sort_emit<4>(cand, (int)ncand0, a, row, gmax);
-    else wave_sort_emit<8>(cand, (int)ncand0, a, row, gmax);
-    return;
-  }
-
-  // ---- exact running top-K over the candidates and the enumerated segments ----
   for (int i = tid; i < K; i += kSelectThreads) sel[i] = 0ull;
+  if (tid == 0) misc[M_BUF] = 0u;
   __syncthreads();
   auto merge = [&](int nb) {
     rr_rescore_any(cand, nb, a, qs);
@@ -324,29 +478,11 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     if (tid == 0) misc[M_BUF] = 0u;
     __syncthreads();
   };
-  if (tid == 0) misc[M_BUF] = 0u;
-  __syncthreads();
-  if (full_scan) {  // too many candidates or segments: enumerate every eligible item of the row
-    ls_stream(allseg, allpre, 2, cand, misc, a.gid0, n, kLsFlush, elig_bit, merge);
-  } else {
-    if (ncand0) merge((int)ncand0);  // the complete lists' candidates (<= kLsCand / 2) first
-    if (nseg) {
-      if (tid == 0) {
-        uint32_t acc = 0;
-        for (uint32_t s = 0; s < nseg; ++s) {
-          pre[s] = acc;
-          acc += (seg[2 * s + 1] >> 1) * 16;
-        }
-        pre[nseg] = acc;
-        misc[M_BUF] = 0u;
-      }
-      __syncthreads();
-      ls_stream(seg, pre, (int)nseg, cand, misc, a.gid0, n, kLsFlush, elig_bit, merge);
-    }
-  }
+  ls_stream(allseg, allpre, 2, cand, misc, a.gid0, n, kLsFlush, elig_bit, merge);
   // ---- emit the running list (rank 0 dropped when it heads it) ----
   int cnt = 0;
   for (int i = 0; i < K; ++i) cnt += sel[i] != 0ull;  // uniform: every thread counts
+  if (a.trace && tid == 0) a.trace[row * 16 + 10] = 1;
   if (a.out_scores) {
     const int start = (gmax && cnt && sel[0] == gmax) ? 1 : 0;
     const int c = min(a.k_final, cnt - start);

@@ -317,11 +317,18 @@ template <int CPL, int U, int NG>
 __device__ __forceinline__ void rescore_rows(uint64_t* keys, int m, const SelectArgs& a, const float* qs, int t) {
   const int p = t & 15, g = t >> 4;
   const int nch = a.rr_d >> 2;
-  f4v qv[CPL];
+  // the query chunks of this lane in f64 (zero past the row: those FMAs add exact zeros, so
+  // the sum — and its order — is the same for every row width; no per-chunk branches, which
+  // put every FMA in a basic block of its own behind its own s_waitcnt)
+  double qd[CPL][4];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
     const int c = p + 16 * j;
-    qv[j] = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
+    const f4v q = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
+    qd[j][0] = (double)q.x;
+    qd[j][1] = (double)q.y;
+    qd[j][2] = (double)q.z;
+    qd[j][3] = (double)q.w;
   }
   for (int c0 = g * U; c0 < m; c0 += NG * U) {
     uint32_t gid[U];
@@ -337,13 +344,12 @@ __device__ __forceinline__ void rescore_rows(uint64_t* keys, int m, const Select
     for (int u = 0; u < U; ++u) {
       double acc = 0.0;
 #pragma unroll
-      for (int j = 0; j < CPL; ++j)
-        if (p + 16 * j < nch) {
-          acc = fma((double)xv[u][j].x, (double)qv[j].x, acc);
-          acc = fma((double)xv[u][j].y, (double)qv[j].y, acc);
-          acc = fma((double)xv[u][j].z, (double)qv[j].z, acc);
-          acc = fma((double)xv[u][j].w, (double)qv[j].w, acc);
-        }
+      for (int j = 0; j < CPL; ++j) {
+        acc = fma((double)xv[u][j].x, qd[j][0], acc);
+        acc = fma((double)xv[u][j].y, qd[j][1], acc);
+        acc = fma((double)xv[u][j].z, qd[j][2], acc);
+        acc = fma((double)xv[u][j].w, qd[j][3], acc);
+      }
       acc = sum16_f64(acc);
       if (p == 0 && c0 + u < m) keys[c0 + u] = rr_key((float)acc, gid[u]);
     }

@@ -166,9 +166,12 @@ int bb_search(bb_index* idx, const bb_query* q, bb_result* res);
 /* Lengths of the BB_Q_OUT_KEYS lists for a query: sides (1 or 2) and k_int per side. */
 int bb_key_lens(const bb_query* q, int32_t* sides, int32_t* k_int);
 
-/* Cross-shard merge: keys gathered from P shards ([P][sides][B][k_int], device) and
- * their max_keys ([P][B], device) -> final results, applying the same rank-0 drop,
- * truncation and hybrid blend bb_search applies locally. */
+/* Cross-shard merge: keys gathered from P shards ([P][sides][B][k_int]) and their
+ * max_keys ([P][B]) -> final results, applying the same rank-0 drop, truncation and
+ * hybrid blend bb_search applies locally.  keys / max_keys live where
+ * q->where says (host lists are staged to the device); results where res->where says.
+ * BB_Q_OUT_KEYS searches write their lists to host buffers too when res->where is
+ * BB_HOST (synchronised before returning). */
 int bb_finalize(bb_index* idx, const bb_query* q, const uint64_t* keys, const uint64_t* max_keys,
                 int32_t n_parts, bb_result* res);
 
