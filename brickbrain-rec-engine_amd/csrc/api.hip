@@ -16,6 +16,7 @@
 
 #include "../../include/brickrec.h"
 #include "common.h"
+#include "list_epi.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -676,20 +677,21 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   const bool rr_c = !no_rr && !stream && n_slabs == 1 && need_content && x->items_bf.p;
   const bool rr_f = !no_rr && !stream && n_slabs == 1 && need_cf && x->cf_bf.p;
   // Bounded candidate lists (list_epi.h, select_list.hip) on the re-rank scans: no score
-  // image; per lane the top-4 keys of every period of G tiles.  Geometry of a query chunk of
-  // bpad_c rows: item chunks of the scan launch, periods per chunk (enough lists that a list
-  // expects <= 1/3 of a top-K member: 2·chunks·periods >= 3·K_int), tiles per period.
+  // image; per lane the top-5 keys of every period of G <= 8 tiles.  Geometry of a query
+  // chunk of bpad_c rows: item chunks of the scan launch (scan2 or scan4), periods per chunk
+  // (enough lists that a list expects <= 1/3 of a top-K member: 2·chunks·periods >= 3·K_int),
+  // tiles per period.
   auto list_geom = [&](int bpad_c, int& nch, int& np, int& G) -> bool {
-    if (x->lists_opt == 0 || scan4_used(BF16, bpad_c)) return false;
+    if (x->lists_opt == 0) return false;
     const int tiles = (int)(round_up(x->n, kTileRows) / 32);
-    nch = scan_n_chunks(bpad_c, tiles);
+    nch = scan_chunks(BF16, bpad_c, tiles, false);
     const int tpc = (tiles + nch - 1) / nch;
-    if (tpc > 2047 || nch > 256) return false;
-    np = 1;
+    if (nch > 256) return false;
+    np = (tpc + kListMaxPeriod - 1) / kListMaxPeriod;
     while (2 * nch * np < 3 * K_int && 2 * nch * (np + 1) <= 1024 && np < tpc) ++np;
     G = (tpc + np - 1) / np;
     np = (tpc + G - 1) / G;
-    return 2 * nch * np <= 1024;
+    return G <= kListMaxPeriod && 2 * nch * np <= 1024;
   };
 
   // stage host inputs
@@ -928,7 +930,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // BB_DUAL=0 (A/B runs) keeps one launch per side.
     static const bool dual_env = !(getenv("BB_DUAL") && atoi(getenv("BB_DUAL")) == 0);
     static const int sel_wave_env0 = getenv("BB_SELECT_WAVE") ? atoi(getenv("BB_SELECT_WAVE")) : -1;
-    const bool dual = dual_env && q->mode == BB_MODE_HYBRID && sides == 2 && s16_c && s16_f && !stream &&
+    const bool dual = dual_env && q->mode == BB_MODE_HYBRID && sides == 2 && ((s16_c && s16_f) || (list_c && list_f)) &&
+                      !stream &&
                       n_slabs == 1 && scan4_used(BF16, bpad) && scan4_dual_supported((int)x->Dpad_b / 8, (int)x->Rpad_b / 8) &&
                       std::min<int64_t>(slab, x->n) <= 32768 && K_int <= 256 && sel_wave_env0 != 0 && bc > 256;
     if (dual && (rc = x->rr_flags.ensure((size_t)Bc * 4 * 2))) return rc;

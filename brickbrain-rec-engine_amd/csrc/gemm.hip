@@ -25,6 +25,7 @@
 
 #include "gemm_kernel.h"
 #include "scan3_kernel.h"
+#include "list_epi.h"
 
 namespace bb {
 
@@ -144,9 +145,10 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   // the int16 score image: bf16 scans of rows up to kRrMaxD, slab epilogue only
   if (a.s_h && (dtype != BF16 || a.cand || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.Kpad > kRrMaxD))
     return hipErrorInvalidValue;
-  // candidate lists: the bf16 scan2 of a re-rank search (query chunks the scan4 does not take)
-  if (a.lists && (!a.s_h || a.q_istats || scan4_used(BF16, a.Mpad) || a.l_period <= 0 || a.l_np <= 0 ||
-                  (int64_t)a.l_period * a.l_np * scan_n_chunks(a.Mpad, a.Ncols / 32) < a.Ncols / 32))
+  // candidate lists: the bf16 scans of a re-rank search (rows up to kRrMaxD wide), periods of
+  // at most kListMaxPeriod tiles covering every chunk
+  if (a.lists && (!a.s_h || a.q_istats || a.cand || a.l_period <= 0 || a.l_period > kListMaxPeriod || a.l_np <= 0 ||
+                  (int64_t)a.l_period * a.l_np * scan_chunks(BF16, a.Mpad, a.Ncols / 32, false) < a.Ncols / 32))
     return hipErrorInvalidValue;
   if (gemm_uses_scan(dtype, a.Mpad, a.Kpad)) {
     if (dtype == BF16 ? launch_scan<uint16_t>(a, s) : launch_scan<float>(a, s)) return hipGetLastError();

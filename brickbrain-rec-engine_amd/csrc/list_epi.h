@@ -2,16 +2,18 @@
 //
 // Replaces the score image of the exact re-rank path (one slab, f32 index: every 25K-row
 // config).  Instead of writing B×N int16 codes that a select kernel re-reads, each lane keeps
-// the top-4 keys of its own items in registers and writes them once per list period:
+// the top-5 keys of its own items in registers and writes them once per list period:
 //
 //   key  = (code << 16) | pos          code = u16 image of the approximate score,
 //                                      c = round(65535·(0.5 + s/(65535·h))) ≈ 32767.5 + s/h
-//                                      pos  = item offset inside the workgroup's item chunk
-//   list = the 4 largest keys over the lane's eligible items of one period (G tiles × 16 items)
+//                                      pos  = (tile within the period << 4) | accumulator
+//                                      register g (item (g & 3) + 8 (g >> 2) + 4·half)
+//   list = the 5 largest keys over the lane's eligible items of one period (G <= 8 tiles ×
+//          16 items), packed into 128 bits: five codes + five 7-bit positions (list_pack5)
 //
 // The select (select_list.hip) bounds the K-th approximate score by the K-th largest list
-// head, takes every key within the re-rank margin of it, and enumerates exhaustively only the
-// lists whose 4th key still lies inside the margin (they may have dropped a candidate).
+// key, takes every key within the re-rank margin of it, and enumerates exhaustively only the
+// lists whose 5th key still lies inside the margin (they may have dropped a candidate).
 // Rank 0 (similar / hybrid content side): the top-2 present half-tile maxima per lane and
 // item chunk, (code << 16) | tile offset.
 //
@@ -37,18 +39,41 @@ __device__ __forceinline__ uint32_t list_codes(float a, float b, float k2) {
   return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_u16(fmaf(a, k2, 0.5f), fmaf(b, k2, 0.5f)));
 }
 
-// per-lane sorted top-4 (k0 >= k1 >= k2 >= k3): one max + three med3, no dependent chain
-struct ListTop4 {
-  uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+// per-lane sorted top-5 (k0 >= ... >= k4): one max + four med3, no dependent chain
+struct ListTop5 {
+  uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0, k4 = 0;
   __device__ __forceinline__ void ins(uint32_t x) {
-    const uint32_t n0 = maxu(k0, x), n1 = med3u(k0, k1, x), n2 = med3u(k1, k2, x), n3 = med3u(k2, k3, x);
+    const uint32_t n0 = maxu(k0, x), n1 = med3u(k0, k1, x), n2 = med3u(k1, k2, x), n3 = med3u(k2, k3, x),
+                   n4 = med3u(k3, k4, x);
     k0 = n0;
     k1 = n1;
     k2 = n2;
     k3 = n3;
+    k4 = n4;
   }
-  __device__ __forceinline__ void reset() { k0 = k1 = k2 = k3 = 0u; }
+  __device__ __forceinline__ void reset() { k0 = k1 = k2 = k3 = k4 = 0u; }
+  // 128 bits: x = c0:c1, y = c2:c3, z = c4 : p0 (7 b) : p1 (7 b), w = p2 : p3 : p4 (7 b each)
+  __device__ __forceinline__ uint4 pack() const {
+    return make_uint4((k0 & 0xFFFF0000u) | (k1 >> 16), (k2 & 0xFFFF0000u) | (k3 >> 16),
+                      (k4 & 0xFFFF0000u) | ((k0 & 0x7Fu) << 7) | (k1 & 0x7Fu),
+                      ((k2 & 0x7Fu) << 14) | ((k3 & 0x7Fu) << 7) | (k4 & 0x7Fu));
+  }
 };
+// unpacked list: codes c[0..4] (descending) and positions p[0..4]
+__host__ __device__ inline void list_unpack5(uint4 v, uint32_t c[5], uint32_t p[5]) {
+  c[0] = v.x >> 16;
+  c[1] = v.x & 0xFFFFu;
+  c[2] = v.y >> 16;
+  c[3] = v.y & 0xFFFFu;
+  c[4] = v.z >> 16;
+  p[0] = (v.z >> 7) & 0x7Fu;
+  p[1] = v.z & 0x7Fu;
+  p[2] = (v.w >> 14) & 0x7Fu;
+  p[3] = (v.w >> 7) & 0x7Fu;
+  p[4] = v.w & 0x7Fu;
+}
+constexpr int kListMaxPeriod = 8;  // tiles per period: 7-bit positions
+
 struct ListTop2 {
   uint32_t k0 = 0, k1 = 0;
   __device__ __forceinline__ void ins(uint32_t x) {
@@ -58,17 +83,14 @@ struct ListTop2 {
   }
 };
 
-// pos of accumulator register pair p (registers 2p, 2p+1) of lane half h in tile offset t:
-// register g <-> item (g & 3) + 8 (g >> 2) + 4h of the tile; both positions of the pair in
-// one word (lo = register 2p, hi = 2p + 1): pb2 + list_pair_pos(p), pb2 = pb·0x10001,
-// pb = (t << 5) | (h << 2)
-__host__ __device__ constexpr uint32_t list_pair_pos(int p) {
-  return (uint32_t)((p & 1) * 2 + 8 * (p >> 1)) * 0x10001u + 0x10000u;
-}
+// positions of accumulator register pair p (registers 2p, 2p+1) of tile t of the period,
+// both in one word (lo = register 2p, hi = 2p + 1): list_pb2(t) + list_pair_pos(p)
+__host__ __device__ constexpr uint32_t list_pair_pos(int p) { return (uint32_t)(2 * p) * 0x10001u + 0x10000u; }
+__host__ __device__ constexpr uint32_t list_pb2(int t_in_period) { return (uint32_t)(t_in_period << 4) * 0x10001u; }
 
 // Insert one register pair of a half tile.  e16: bit g = register g eligible (ignored when
 // full).  Masked registers get code 0 (their keys sort below every real key).
-__device__ __forceinline__ void list_pair(ListTop4& L, float a, float b, float k2, uint32_t pb2, int p, bool full,
+__device__ __forceinline__ void list_pair(ListTop5& L, float a, float b, float k2, uint32_t pb2, int p, bool full,
                                           uint32_t e16) {
   uint32_t w = list_codes(a, b, k2);
   if (!full) {

@@ -413,7 +413,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     sk = hq > 0.f ? 1.0f / (hq * 32767.f) : 0.f;
     asm volatile("" : "+v"(sk));  // consumed before any LDS-DMA is in flight
   }
-  // bounded candidate lists (list_epi.h): code scale k2 = 1/(65535·h), the lane's top-4 of
+  // bounded candidate lists (list_epi.h): code scale k2 = 1/(65535·h), the lane's top-5 of
   // the current period, the rank-0 top-2, the period counters (wave-uniform)
   constexpr bool LIST = (ABL & kScanList) != 0 && !STREAM && !S16;
   float k2 = 0.f;
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     k2 = hq > 0.f ? 1.0f / (hq * 65535.f) : 0.f;
     asm volatile("" : "+v"(k2));  // consumed before any LDS-DMA is in flight
   }
-  ListTop4 lst;
+  ListTop5 lst;
   ListTop2 r0l;
   uint32_t l_e16 = 0, l_pb2 = 0, l_kodd = 0;
   bool l_full = true;
@@ -431,8 +431,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   const bool l_live = __any(q < a.M_valid);  // padded query blocks store nothing
   auto list_store = [&]() __attribute__((always_inline)) {
     if (l_live)
-      *(uint4*)(a.lists + 4 * list_slot(chunk, l_period, a.l_np, l_nb, l_blk, lane)) =
-          make_uint4(lst.k0, lst.k1, lst.k2, lst.k3);
+      *(uint4*)(a.lists + 4 * list_slot(chunk, l_period, a.l_np, l_nb, l_blk, lane)) = lst.pack();
     lst.reset();
     l_cnt = 0;
     ++l_period;
@@ -503,7 +502,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
           asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[u]));
       }
       if constexpr (u > 0) asm volatile("" ::"v"(__builtin_bit_cast(u32x4v, fq[(u + 3) % 4])));
-      // ---- list epilogue (kScanList): eligibility, 16 half-pair slices (codes, keys, top-4
+      // ---- list epilogue (kScanList): eligibility, 16 half-pair slices (codes, keys, top-5
       // inserts), rank 0, the period store, then the next tile's words and staging ----
       if constexpr (LIST) {
         constexpr int kLS = 20 + PIECES;
@@ -514,7 +513,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
               if constexpr (epi) {
                 l_e16 = list_elig16(pw & mw & ~ew, ptile0, a.n_valid, h);
                 l_full = __all(l_e16 == 0xFFFFu);
-                l_pb2 = ((uint32_t)(((ptile - tile_lo) << 5) | (h << 2))) * 0x10001u;
+                l_pb2 = list_pb2(l_cnt);  // ptile's place in the period
               }
             } else if constexpr (s <= 16) {
               if constexpr (epi) {
@@ -629,7 +628,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     if constexpr (LIST) {
       const uint32_t e16 = list_elig16(pw & mw & ~ew, tile * 32, a.n_valid, h);
       const bool full = __all(e16 == 0xFFFFu);
-      const uint32_t pb2 = ((uint32_t)(((tile - tile_lo) << 5) | (h << 2))) * 0x10001u;
+      const uint32_t pb2 = list_pb2(l_cnt);
 #pragma unroll
       for (int pp = 0; pp < 8; ++pp) list_pair(lst, p[2 * pp], p[2 * pp + 1], k2, pb2, pp, full, e16);
       if (a.r0lists) {

@@ -30,6 +30,7 @@
 // streaming epilogue (kScanStream) appending candidates to per-lane regions
 // ((q·n_chunks + chunk)·2 + h, one region set per query as before).
 #pragma once
+#include "list_epi.h"
 #include "scan2_kernel.h"
 
 namespace bb {
@@ -227,6 +228,29 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     skA = hA > 0.f ? 1.0f / (hA * 32767.f) : 0.f;
     skB = hB > 0.f ? 1.0f / (hB * 32767.f) : 0.f;
   }
+  // bounded candidate lists (kScanList, list_epi.h; interleaved schedule only): per block the
+  // code scale 1/(65535·h), the lane's top-5 of the current period and the rank-0 top-2.  A
+  // finished period's lists are packed and stored at the start of the NEXT tile body, ahead
+  // of its DMA pieces, so the end-of-tile vmcnt wait never waits for a store's round trip.
+  constexpr bool LIST = (ABL & kScanList) != 0 && !STREAM && !S16;
+  static_assert(!LIST || IL, "list epilogue: interleaved schedule (rows up to 512 wide) only");
+  float k2A = 0.f, k2B = 0.f;
+  if constexpr (LIST) {
+    const float hA = qA < a.M_valid ? a.s_h[qA] : 0.f, hB = qB < a.M_valid ? a.s_h[qB] : 0.f;
+    k2A = hA > 0.f ? 1.0f / (hA * 65535.f) : 0.f;
+    k2B = hB > 0.f ? 1.0f / (hB * 65535.f) : 0.f;
+  }
+  ListTop5 lstA, lstB;
+  ListTop2 r0A, r0B;
+  uint4 pendA = make_uint4(0u, 0u, 0u, 0u), pendB = make_uint4(0u, 0u, 0u, 0u);
+  bool pend = false;
+  int l_cnt = 0, l_period = 0, pend_period = 0;
+  const int l_nb = a.Mpad >> 5;
+  const bool liveA = __any(qA < a.M_valid), liveB = __any(qB < a.M_valid);  // padded blocks store nothing
+  auto list_put = [&](int period, const uint4& vA, const uint4& vB) __attribute__((always_inline)) {
+    if (liveA) *(uint4*)(a.lists + 4 * list_slot(chunk, period, a.l_np, l_nb, qA >> 5, lane)) = vA;
+    if (liveB) *(uint4*)(a.lists + 4 * list_slot(chunk, period, a.l_np, l_nb, qB >> 5, lane)) = vB;
+  };
   Stream4 slA, slB;
   auto region = [&](int q) __attribute__((always_inline)) { return ((size_t)q * n_chunks + chunk) * 2 + h; };
   if constexpr (STREAM) {  // bound = the last key of the query's pilot list (stream_begin)
@@ -255,6 +279,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   asm volatile("" : "+v"(pw), "+v"(mw), "+v"(ewA), "+v"(ewB));
   if constexpr (STREAM) asm volatile("" : "+v"(slA.thr), "+v"(slB.thr), "+v"(slA.thrf), "+v"(slB.thrf));
   if constexpr (S16) asm volatile("" : "+v"(skA), "+v"(skB));
+  if constexpr (LIST) asm volatile("" : "+v"(k2A), "+v"(k2B));
   asm volatile("s_nop 4");
 
   f32x16s accA = {}, accB = {};
@@ -320,12 +345,45 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     }
   };
   constexpr int kEpi = 7;
+  // List epilogue of one block's tile (kLE slices): 0 eligibility, 1..16 the eight register
+  // pairs (codes + masked keys + two top-5 inserts, one insert per slice), 17 rank 0.
+  constexpr int kLE = 18;
+  auto list_slice = [&](auto SS, const f32x16s& p, int ptile, uint32_t epw, uint32_t emw, uint32_t eew, float k2,
+                        ListTop5& L, ListTop2& R, uint32_t& e16, bool& full, uint32_t& kodd) __attribute__((always_inline)) {
+    constexpr int s = decltype(SS)::value;
+    const int ptile0 = ptile * 32;
+    if constexpr (s == 0) {
+      e16 = list_elig16(epw & emw & ~eew, ptile0, a.n_valid, h);
+      full = __all(e16 == 0xFFFFu);
+    } else if constexpr (s <= 16) {
+      constexpr int pp = (s - 1) >> 1;
+      if constexpr (((s - 1) & 1) == 0) {
+        uint32_t w = list_codes(p[2 * pp], p[2 * pp + 1], k2);
+        if (!full) {
+          const uint32_t lo = 0u - ((e16 >> (2 * pp)) & 1u), hi = 0u - ((e16 >> (2 * pp + 1)) & 1u);
+          w &= (lo & 0xFFFFu) | (hi & 0xFFFF0000u);
+        }
+        const uint32_t ix = list_pb2(l_cnt) + list_pair_pos(pp);
+        L.ins(__builtin_amdgcn_perm(w, ix, 0x05040100u));
+        kodd = __builtin_amdgcn_perm(w, ix, 0x07060302u);
+      } else {
+        L.ins(kodd);
+      }
+    } else if constexpr (s == 17) {
+      if (a.r0lists) {
+        const float m = list_present_max(p, list_elig16(epw, ptile0, a.n_valid, h));
+        R.ins(list_r0_key(m, k2, (uint32_t)(ptile - tile_lo)));
+      }
+    }
+  };
+  uint32_t le16A = 0, le16B = 0, lkoA = 0, lkoB = 0;
+  bool lfullA = true, lfullB = true;
   // slice placement inside a chain: epilogue slices from u = 2 (after the tie of the other
   // accumulator), then (chain A) the next tile's words and staging pieces
   constexpr int kSlicesA = PIECES + 1 + kEpi;
   // End of a tile: wait for the LDS-DMA of the next tile, not for block A's score-image
   // stores issued after it (vmcnt counts loads, stores and LDS-DMA together, in order).
-  constexpr bool kStores = !STREAM && !(ABL & (1 | 8));
+  constexpr bool kStores = !STREAM && !LIST && !(ABL & (1 | 8));
 
   // One tile: chain A over buffer BUF (+ block B's epilogue of tile-1 when EPIB), chain B
   // (+ block A's epilogue of this tile).
@@ -461,6 +519,54 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
           asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[b * U + u]));
         if constexpr (b == 0 && u > 0) asm volatile("" ::"v"(fq[(u + 3) % 4]));
         if constexpr (st == 1 && epi) asm volatile("s_nop 15" : "+v"(pA), "+v"(pB));
+        if constexpr (LIST) {
+          // slices: the pending period store (step 0, ahead of the DMA), DMA pieces (even
+          // steps from 2), the next tile's words, then the previous tile's list epilogue of
+          // block A and block B (odd steps between the pieces, then one per step) and the
+          // period counter
+          constexpr int kE = 2 * kLE + 1;
+          static_for<PIECES + 2 + kE>([&](auto SL) {
+            constexpr int s = decltype(SL)::value;
+            constexpr int e = s - PIECES - 2;  // epilogue slice index (s >= PIECES + 2)
+            constexpr int at0 = s == 0 ? 0 : s <= PIECES ? 2 * s : s == PIECES + 1 ? 2 * PIECES + 2
+                                : e < PIECES ? 3 + 2 * e : 2 * PIECES + 3 + (e - PIECES);
+            constexpr int at = at0 < 2 * U ? at0 : 2 * U - 1;
+            if constexpr (at == st) {
+              if constexpr (s == 0) {
+                if (pend) {
+                  list_put(pend_period, pendA, pendB);
+                  pend = false;
+                }
+              } else if constexpr (s <= PIECES) {
+                stage_piece(stile, buf ^ 1, s - 1);
+              } else if constexpr (s == PIECES + 1) {
+                nw_p = a.present[w0 + wtile];
+                nw_m = a.mask[w0 + wtile];
+                nw_eA = erowA[w0 + wtile];
+                nw_eB = erowB[w0 + wtile];
+              } else if constexpr (epi) {
+                if constexpr (e < kLE) {
+                  list_slice(std::integral_constant<int, e>{}, pA, tile - 1, ppw, pmw, pewA, k2A, lstA, r0A, le16A, lfullA,
+                             lkoA);
+                } else if constexpr (e < 2 * kLE) {
+                  list_slice(std::integral_constant<int, e - kLE>{}, pB, tile - 1, ppw, pmw, pewB, k2B, lstB, r0B, le16B,
+                             lfullB, lkoB);
+                } else {
+                  if (++l_cnt == a.l_period) {
+                    pendA = lstA.pack();
+                    pendB = lstB.pack();
+                    pend = true;
+                    pend_period = l_period++;
+                    lstA.reset();
+                    lstB.reset();
+                    l_cnt = 0;
+                  }
+                }
+              }
+            }
+          });
+          return;
+        }
         // slices: DMA pieces (every other step from st = 2), the next tile's words, then
         // the previous tile's epilogue of block A and of block B
         constexpr int kS = PIECES + 1 + 2 * kEpi;
@@ -516,6 +622,21 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     // both blocks' epilogues of the last tile (not overlapped)
     auto last = [&](f32x16s& lA, f32x16s& lB) __attribute__((always_inline)) {
       asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" : "+v"(lA), "+v"(lB));
+      if constexpr (LIST) {
+        if (pend) list_put(pend_period, pendA, pendB);
+        static_for<kLE>([&](auto SL) {
+          list_slice(SL, lA, tile - 1, ppw, pmw, pewA, k2A, lstA, r0A, le16A, lfullA, lkoA);
+        });
+        static_for<kLE>([&](auto SL) {
+          list_slice(SL, lB, tile - 1, ppw, pmw, pewB, k2B, lstB, r0B, le16B, lfullB, lkoB);
+        });
+        if (a.r0lists) {
+          if (liveA) *(uint2*)(a.r0lists + 2 * list_slot(chunk, 0, 1, l_nb, qA >> 5, lane)) = make_uint2(r0A.k0, r0A.k1);
+          if (liveB) *(uint2*)(a.r0lists + 2 * list_slot(chunk, 0, 1, l_nb, qB >> 5, lane)) = make_uint2(r0B.k0, r0B.k1);
+        }
+        list_put(l_period, lstA.pack(), lstB.pack());  // the last (possibly partial) period
+        return;
+      }
       uint32_t te = 0, tp = 0, ep = 0;
       bool any = false;
       static_for<kEpi>([&](auto SL) { epi_slice(SL, lA, tile - 1, ppw, pmw, pewA, qA, slA, te, tp, ep, any); });

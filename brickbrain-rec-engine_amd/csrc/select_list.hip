@@ -5,13 +5,13 @@
 // (recommendation_system.py:214-247), the CF loop + sort (:438-461) and pgvector's
 // ORDER BY <=> LIMIT k — for the 25K-row configs.  One workgroup (4 waves) per query row:
 //
-//   lists   every lane's top-4 keys per period (list_epi.h): key = (u16 code, chunk position)
+//   lists   every lane's top-5 keys per period (list_epi.h), packed: u16 codes + 7-bit positions
 //   bound   T0 = the K-th largest code over ALL list keys (two-level histogram): K distinct
 //           items have codes >= T0, so the exact K-th score is >= dec(T0) − ε', and every
 //           exact top-K member has code >= Tg = T0 − Δ (Δ = the re-rank margin
 //           2ε'(1+2^-10)+2^-20 in codes, + 2 codes of slack)
-//   gather  keys >= Tg of the lists whose 4th key is below Tg (they dropped nothing that
-//           matters); a list whose 4th key reaches Tg may have dropped candidates, so every
+//   gather  keys >= Tg of the lists whose 5th key is below Tg (they dropped nothing that
+//           matters); a list whose 5th key reaches Tg may have dropped candidates, so every
 //           eligible item of its period joins the buffer instead (an overflowed list: a few
 //           rows per batch at configs[1])
 //   rank 0  (similar / hybrid content side) the present half tiles whose maximum is within Δ
@@ -123,7 +123,6 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   float* qs = (float*)(dsm + kLsOffQs);
   uint32_t* misc = (uint32_t*)(dsm + kLsOffMisc);
   uint32_t* scan_sh = (uint32_t*)(dsm + kLsOffScan);
-  uint32_t* fb = scan_sh + 4;                        // find_bin results
   uint32_t* allseg = (uint32_t*)(dsm + kLsOffAll);  // both halves of every tile
   uint32_t* allpre = allseg + 4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -198,9 +197,10 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     for (int i = 0; i < kLPT; ++i) {
       if (i < nlw) {
         cnt += (uint32_t)__popcll(__ballot((v[i].x >> 16) >= c));
+        cnt += (uint32_t)__popcll(__ballot((v[i].x & 0xFFFFu) >= c));
         cnt += (uint32_t)__popcll(__ballot((v[i].y >> 16) >= c));
+        cnt += (uint32_t)__popcll(__ballot((v[i].y & 0xFFFFu) >= c));
         cnt += (uint32_t)__popcll(__ballot((v[i].z >> 16) >= c));
-        cnt += (uint32_t)__popcll(__ballot((v[i].w >> 16) >= c));
       }
     }
     return cnt;
@@ -210,9 +210,10 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     uint32_t hi = 0, lo = 0xFFFFu;
 #pragma unroll
     for (int i = 0; i < kLPT; ++i) {
-      hi = max(hi, v[i].x >> 16);  // keys are sorted within a list: x is the largest
-      const uint32_t w = v[i].w >> 16, z = v[i].z >> 16, y = v[i].y >> 16, xx = v[i].x >> 16;
-      const uint32_t mn = w ? w : z ? z : y ? y : xx;
+      hi = max(hi, v[i].x >> 16);  // codes are sorted within a list: c0 is the largest
+      const uint32_t c4 = v[i].z >> 16, c3 = v[i].y & 0xFFFFu, c2 = v[i].y >> 16, c1 = v[i].x & 0xFFFFu,
+                     c0 = v[i].x >> 16;
+      const uint32_t mn = c4 ? c4 : c3 ? c3 : c2 ? c2 : c1 ? c1 : c0;
       lo = mn ? min(lo, mn) : lo;
     }
 #pragma unroll
@@ -258,11 +259,12 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
 #pragma unroll
   for (int i = 0; i < kLPT; ++i) {
     if (i >= nlw) continue;  // wave-uniform
-    const bool live = vt0[i] >= 0 && v[i].x != 0u;
+    uint32_t cc[5], pp[5];
+    list_unpack5(v[i], cc, pp);
+    const bool live = vt0[i] >= 0 && cc[0] != 0u;
     const int j = tid + i * kSelectThreads, hh = j & 1;
     const int c = live ? (j >> 1) / NP : 0;
-    const int tlo = live ? chunk_tile_lo(c, T, NC) : 0;
-    const bool ovf = live && (v[i].w >> 16) >= Tg;  // all four within the margin: the period may hold more
+    const bool ovf = live && cc[4] >= Tg;  // all five within the margin: the period may hold more
     if (ovf) {
       const uint32_t sidx = atomicAdd(&misc[M_SEG], 1u);
       const int thi = chunk_tile_lo(c + 1, T, NC), nt = min(G, thi - vt0[i]);
@@ -272,21 +274,26 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
         seg[2 * sidx + 1] = ((uint32_t)nt << 1) | (uint32_t)hh;
       }
     }
-    // keys are sorted: the ones at or above Tg form a prefix
-    const uint32_t m = live && !ovf ? (uint32_t)((v[i].x >> 16) >= Tg) + (uint32_t)((v[i].y >> 16) >= Tg) +
-                                          (uint32_t)((v[i].z >> 16) >= Tg)
+    // codes are sorted: the keys at or above Tg form a prefix (at most 4 when not overflowed)
+    const uint32_t m = live && !ovf ? (uint32_t)(cc[0] >= Tg) + (uint32_t)(cc[1] >= Tg) + (uint32_t)(cc[2] >= Tg) +
+                                          (uint32_t)(cc[3] >= Tg)
                                     : 0u;
-    const uint64_t b0 = __ballot(m & 1u), b1 = __ballot((m >> 1) & 1u);
-    const uint32_t tot = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1);
+    const uint64_t b0 = __ballot(m & 1u), b1 = __ballot((m >> 1) & 1u), b2 = __ballot((m >> 2) & 1u);
+    const uint32_t tot = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
     if (!tot) continue;
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(&misc[M_CAND], tot);
     base = (uint32_t)__shfl((int)base, 0);
-    const uint32_t p0 = base + (uint32_t)__popcll(b0 & lt_mask) + 2u * (uint32_t)__popcll(b1 & lt_mask);
-    const uint32_t gb = a.gid0 + (uint32_t)(tlo * 32);
-    if (m > 0 && p0 < (uint32_t)kLsCand) cand[p0] = make_key(1u, gb + (v[i].x & 0xFFFFu));
-    if (m > 1 && p0 + 1 < (uint32_t)kLsCand) cand[p0 + 1] = make_key(1u, gb + (v[i].y & 0xFFFFu));
-    if (m > 2 && p0 + 2 < (uint32_t)kLsCand) cand[p0 + 2] = make_key(1u, gb + (v[i].z & 0xFFFFu));
+    const uint32_t p0 = base + (uint32_t)__popcll(b0 & lt_mask) + 2u * (uint32_t)__popcll(b1 & lt_mask) +
+                        4u * (uint32_t)__popcll(b2 & lt_mask);
+    // position -> item: tile vt0 + (pos >> 4), register g = pos & 15 of lane half hh
+    const uint32_t gb = a.gid0 + (uint32_t)(vt0[i] * 32 + 4 * hh);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t g = pp[e] & 15u;
+      const uint32_t item = (pp[e] >> 4) * 32u + (g & 3u) + 8u * (g >> 2);
+      if ((uint32_t)e < m && p0 + e < (uint32_t)kLsCand) cand[p0 + e] = make_key(1u, gb + item);
+    }
   }
   // rank 0: present half tiles within Δ of the largest present maximum
   if (want_r0) {
