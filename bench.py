@@ -190,6 +190,47 @@ def cpu_baseline(x_np, q_np, k, budget_s=8.0, sweep_s=2.0):
     return out, ids0
 
 
+def cpu_baseline_hybrid(x_np, f_np, mask, liked, rated, u, k, budget_s=10.0, n_sample=64):
+    """configs[2] on the host: the oracle's HybridRecommender scoring path
+    (recommendation_system.py:612-677) per query — liked-set cosine over every item with the
+    rank-0 drop and the mask (:194-249, top 2k), CF u·Fᵀ with rated items and the mask
+    excluded (:411-483, top 2k), union blend 0.4/0.6 (:789-843) — the cosine and CF products
+    batched through numpy/BLAS, timed on a bounded sample of the workload's own queries, on
+    all BLAS threads and on one (the reference deployment's OMP_NUM_THREADS=1)."""
+    from oracle import restatement as R
+    xn = R.normalize_rows(x_np)
+    nq = min(n_sample, len(liked))
+
+    def run(nq_):
+        sim = xn[liked[:nq_]] @ xn.T                       # cosine_similarity(x_t, X), batched
+        fs = u[:nq_] @ f_np.T                              # user_factors[u] · item_factors.T
+        res = []
+        for b in range(nq_):
+            drop = R.rank0(sim[b])
+            okc = mask.copy()
+            okc[drop] = False
+            ci, cs = R.topk_indices(sim[b], 2 * k, okc)
+            fi, fsc = R.topk_indices(fs[b], 2 * k, mask & ~rated[b])
+            res.append(R.union_blend(ci, cs, fi, fsc, 0.4, 0.6, k)[0])
+        return res
+    ids0 = run(nq)
+    out = {"unit": "queries/s", "kind": "port", "cores": int(_blas_threads()),
+           "sample": f"{nq} configs[2] queries per call (the bench's own liked sets, users, mask and rated items) "
+                     f"x {x_np.shape[0]} x {x_np.shape[1]} fp32 + r={f_np.shape[1]} CF: oracle/restatement.py "
+                     f"similar_sets + cf_topk + union_blend semantics, numpy/BLAS, timed"}
+    n_, el, lat = _time_cpu(lambda: run(nq), budget_s, 200)
+    out["value"] = round(n_ * nq / el, 1)
+    out["p50_ms_per_call"] = round(1e3 * float(np.median(lat)), 2)
+    try:
+        from threadpoolctl import threadpool_limits
+        with threadpool_limits(limits=1, user_api="blas"):
+            n1, el1, _ = _time_cpu(lambda: run(nq), budget_s / 2, 100)
+        out["value_1_thread"] = round(n1 * nq / el1, 1)
+    except Exception:
+        pass
+    return out, ids0
+
+
 SHARDED = {  # BASELINE.json configs[3] / configs[4]
     "c4": dict(n=1_000_000, d=768, B=4096, k=100, cfg="configs[3]: 1M synthetic items x 768-d bf16, batch=4096, "
                                                       "top-100, item rows sharded, RCCL top-K merge"),
@@ -335,7 +376,7 @@ def make_lane(brickrec, workload, base, B, local, dev, rank, j, inflight, extra)
         ew = torch.from_numpy(brickrec.bits_from_bool(rated).view(np.int32)).to(dev)
         run, outs = idx.prepared_search("hybrid", TOPK, q_items=torch.from_numpy(liked).to(dev),
                                         q_cf=torch.from_numpy(u).to(dev), mask=mw, excl=ew, stream=s)
-        return idx, s, run, outs, None
+        return idx, s, run, outs, {"liked": liked, "rated": rated, "u": u, "mask": np.asarray(mask, bool)}
     q = unit_rows_torch(B, DIM, 4321 + rank + 1000 * j, dev)
     run, outs = idx.prepared_search("semantic", TOPK, q_rows=q, stream=s)
     return idx, s, run, outs, q
@@ -539,6 +580,13 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_sweep and not hybrid:
         out["gpu_batch_sweep"] = gpu_batch_sweep(brickrec, base, local, dev)
+    if rank == 0 and world == 1 and not args.no_cpu and hybrid:
+        x_np = x.cpu().numpy()
+        cb, ids0 = cpu_baseline_hybrid(x_np, extra["f"], q["mask"], q["liked"], q["rated"], q["u"], TOPK)
+        gpu_ids = o_ids.cpu().numpy()
+        cb["topk_set_agreement_with_gpu"] = round(float(np.mean([set(gpu_ids[i][gpu_ids[i] >= 0]) == set(ids0[i])
+                                                                 for i in range(len(ids0))])), 4)
+        out["cpu_baseline"] = cb
     if rank == 0 and world == 1 and not args.no_cpu and not hybrid:
         x_np = x.cpu().numpy()
         q_np = q.cpu().numpy()

@@ -28,6 +28,13 @@ A rank whose block is empty (N < P·⌈N/P⌉ leaves the last ranks without rows
 4 ranks) uploads nothing and contributes empty key lists (key 0 = empty slot) to the
 gather; it still runs the merge, so every rank returns the same results.
 
+Masks and exclusions cross the interface as per-rank device bitsets: ``mask_bits`` (a
+predicate evaluated on the rank's own attribute columns by ``bb_eval_mask``, or a global
+bool array sliced once) and ``excl_bits`` (per-query item-id lists, e.g. rated sets,
+scattered into [B, words] on the device).  ``search`` takes them as they are — no
+global [N] / [B, N] host array is sliced, packed or copied per call.  Global host arrays
+are still accepted for small cases (tests), at that per-call cost.
+
 At 25K items the index does not shard (39 MB); ``bench.py --gpus N`` runs replicas.
 """
 from __future__ import annotations
@@ -102,6 +109,69 @@ class ShardedIndex:
         self.local.upload_attrs(self._mine(np.asarray(num_parts)), self._mine(np.asarray(year)),
                                 self._mine(np.asarray(theme_id)))
 
+    # ---------------------------------------------------------------- per-rank bitsets
+    @property
+    def n_local(self) -> int:
+        return max(self.hi - self.lo, 0)
+
+    @property
+    def words(self) -> int:
+        return (self.n_local + 31) // 32
+
+    def mask_bits(self, mask=None, *, pred=None):
+        """This rank's item mask as a device bitset (int32 [words]): a ``Predicate`` evaluated
+        on the local attribute columns on the device (``bb_eval_mask``), or a global bool [N]
+        sliced to this rank's rows once (keep the result and pass it to every ``search``)."""
+        import torch
+        dev = self._device()
+        if self.empty:
+            return torch.zeros((0,), dtype=torch.int32, device=dev)
+        if pred is not None:
+            return self.local.eval_mask_bits(pred)
+        from .engine import bits_from_bool
+        loc = np.asarray(mask, bool)
+        loc = loc[self.lo:self.hi] if loc.shape[0] == self.n else loc
+        return torch.as_tensor(bits_from_bool(loc).view(np.int32)).to(dev)
+
+    def excl_bits(self, item_ids):
+        """Per-query exclusions (CF: the user's rated sets, recommendation_system.py:441-451) as
+        a device bitset [B, words] of this rank's rows, scattered on the device from global item
+        ids: a list of B id arrays, or an int64 tensor [B, m] padded with -1.  Ids outside
+        [lo, hi) belong to other ranks and are dropped here; ids within a row must be unique."""
+        import torch
+        dev = self._device()
+        if isinstance(item_ids, torch.Tensor):
+            ids = item_ids.to(dev, torch.int64)
+        else:
+            lists = [np.unique(np.asarray(r, np.int64)) for r in item_ids]
+            m = max([len(r) for r in lists] + [1])
+            pad = np.full((len(lists), m), -1, np.int64)
+            for b, r in enumerate(lists):
+                pad[b, :len(r)] = r
+            ids = torch.from_numpy(pad).to(dev)
+        B, W = int(ids.shape[0]), self.words
+        flat = torch.zeros((B * max(W, 1),), dtype=torch.int64, device=dev)
+        loc = ids - self.lo
+        ok = (ids >= 0) & (loc >= 0) & (loc < self.n_local)
+        rowi = torch.arange(B, device=dev).unsqueeze(1).expand_as(ids)
+        word = (rowi * max(W, 1) + (loc >> 5))[ok]
+        flat.index_add_(0, word, torch.ones_like(word) << (loc[ok] & 31))   # unique ids: sum == or
+        flat = (flat + (1 << 31)) % (1 << 32) - (1 << 31)                  # u32 words as int32
+        return flat.to(torch.int32).view(B, max(W, 1))[:, :W].contiguous()
+
+    def _local_bits(self, a, rows: bool):
+        """A search argument as this rank's device bitset: per-rank int32 words pass through;
+        a global bool host array (small cases) is sliced and packed."""
+        import torch
+        if a is None:
+            return None
+        if isinstance(a, torch.Tensor) and a.dtype == torch.int32 and a.shape[-1] == self.words:
+            return a.to(self._device())
+        from .engine import bits_from_bool
+        g = np.asarray(a.cpu() if isinstance(a, torch.Tensor) else a, bool)
+        loc = g[..., self.lo:self.hi] if g.shape[-1] == self.n else g
+        return torch.as_tensor(bits_from_bool(loc).view(np.int32)).to(self._device())
+
     # ---------------------------------------------------------------- search
     def query_rows(self, item_ids):
         """Rows of global ids, assembled across shards (owner fetch + all-reduce sum)."""
@@ -126,18 +196,15 @@ class ShardedIndex:
     def search(self, mode: str, k: int, *, q_rows=None, q_items=None, q_cf=None, mask=None, excl=None,
                k_side: int = 0, w_content: float = 0.4, w_cf: float = 0.6):
         """Global top-k for a replicated batch; every rank returns the same results.
-        mask: global bool [N] (or None); excl: global bool [B, N] (or None)."""
+        mask: this rank's device bitset (``mask_bits``: int32 [words]) — or a global bool [N]
+        for small cases; excl: this rank's [B, words] device bitset (``excl_bits``) — or a
+        global bool [B, N]."""
         import torch
         dev = self._device()
         if mode in ("similar", "hybrid") and q_rows is None:
             q_rows = self.query_rows(q_items)
-        loc_mask = None if mask is None else torch.as_tensor(np.asarray(mask)[self.lo:self.hi])
-        loc_excl = None if excl is None else torch.as_tensor(np.asarray(excl)[:, self.lo:self.hi])
-        from .engine import bits_from_bool
-        if loc_mask is not None:
-            loc_mask = torch.as_tensor(bits_from_bool(loc_mask.numpy()).view(np.int32)).to(dev)
-        if loc_excl is not None:
-            loc_excl = torch.as_tensor(bits_from_bool(loc_excl.numpy()).view(np.int32)).to(dev)
+        loc_mask = self._local_bits(mask, False)
+        loc_excl = self._local_bits(excl, True)
         q_rows = None if q_rows is None else torch.as_tensor(q_rows).to(dev).float().contiguous()
         q_cf = None if q_cf is None else torch.as_tensor(q_cf).to(dev).float().contiguous()
         if self.empty:   # no rows here: empty lists (key 0) for the gather

@@ -174,6 +174,23 @@ class ItemIndex:
             L.check(self._lib.bb_upload_attrs(self._h, p.ctypes.data, y.ctypes.data, t.ctypes.data),
                     "bb_upload_attrs")
 
+    def eval_mask_bits(self, pred: Predicate):
+        """Evaluate a predicate on the device -> the mask as a device bitset (torch int32
+        [ceil(n/32)] on this index's device), ready to pass to search / search_keys."""
+        import torch
+        ids = np.asarray(list(pred.theme_ids), dtype=np.int64)
+        nbits = int(ids.max()) + 1 if ids.size else 0
+        tb = bits_from_bool(np.isin(np.arange(nbits), ids)) if nbits else np.zeros(1, np.uint32)
+        ex = np.ascontiguousarray(np.asarray(list(pred.excluded_items), dtype=np.int64))
+        bp = L.bb_predicate(int(pred.parts_min), int(pred.parts_max), int(pred.year_min),
+                            int(pred.year_max), int(pred.theme_mode), nbits, tb.ctypes.data,
+                            ex.ctypes.data if ex.size else None, int(ex.size))
+        out = torch.zeros(((self.n_items + 31) // 32,), dtype=torch.int32, device=torch.device("cuda", self.device))
+        torch.cuda.current_stream(out.device).synchronize()
+        with self._mu:
+            L.check(self._lib.bb_eval_mask(self._h, C.byref(bp), out.data_ptr(), L.BB_DEVICE), "bb_eval_mask")
+        return out
+
     def eval_mask(self, pred: Predicate) -> np.ndarray:
         """Evaluate a predicate on the device -> bool mask over the local items."""
         ids = np.asarray(list(pred.theme_ids), dtype=np.int64)

@@ -176,9 +176,20 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     return (size_t)row * ldxb + ch * 16;
   };
   const uint32_t lds_base = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+  // interleaved schedule (d <= 512): the query operand leaves registers for the per-piece
+  // source offsets — precomputed once (each recomputation is ~20 VALU of integer division,
+  // ~130 per tile at d = 384, on a VALU-bound list epilogue)
+  uint32_t soffr[IL ? PIECES : 1];
+  if constexpr (IL) {
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) soffr[p] = (uint32_t)soff(p);
+  }
   // inline asm, as in scan2: the compiler's waitcnt pass must not wait for these
   auto stage_piece = [&](int tile, int buf, int p) __attribute__((always_inline)) {
-    const char* src = Xg + (size_t)tile * 32 * ldxb + soff(p);
+    size_t so;
+    if constexpr (IL) so = soffr[p];
+    else so = soff(p);
+    const char* src = Xg + (size_t)tile * 32 * ldxb + so;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + buf * TILE_B + (wave * PIECES + p) * 1024);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory");
   };

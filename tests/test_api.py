@@ -12,8 +12,9 @@ from _oracle_index import OracleIndex
 from _spaces import catalog_json
 
 
-@pytest.fixture(scope="module")
-def client():
+def make_client(index_factory):
+    """The app over the golden catalogue with the given index (OracleIndex on CPU, None = the
+    HIP ItemIndex); yields a TestClient."""
     pytest.importorskip("httpx")
     from fastapi.testclient import TestClient
     from oracle.gen_golden import PgOnSqlite
@@ -28,11 +29,16 @@ def client():
     old = RS._current_year
     RS._current_year = lambda: year
     try:
-        app = create_app(conn, index_factory=OracleIndex)
+        app = create_app(conn, index_factory=index_factory)
     finally:
         RS._current_year = old
     with TestClient(app) as c:
         yield c
+
+
+@pytest.fixture(scope="module")
+def client():
+    yield from make_client(OracleIndex)
 
 
 def test_health(client):

@@ -53,6 +53,16 @@ def _worker(rank, world, port, out_q):
         res["similar"] = si.search("similar", K, q_items=items, mask=mask)
         res["cf"] = si.search("cf", K, q_cf=torch.from_numpy(u), excl=excl, mask=mask)
         res["hybrid"] = si.search("hybrid", K, q_items=items, q_cf=torch.from_numpy(u), excl=excl, mask=mask)
+        # the scale interface: per-rank bitsets built once (mask sliced once, rated ids
+        # scattered on the rank's device), passed to every search as they are
+        mb = si.mask_bits(mask)
+        eb = si.excl_bits([np.flatnonzero(excl[b]) for b in range(excl.shape[0])])
+        assert mb.dtype == torch.int32 and tuple(mb.shape) == (si.words,)
+        assert eb.dtype == torch.int32 and tuple(eb.shape) == (excl.shape[0], si.words)
+        res["semantic/bits"] = si.search("semantic", K, q_rows=torch.from_numpy(q), mask=mb)
+        res["similar/bits"] = si.search("similar", K, q_items=items, mask=mb)
+        res["cf/bits"] = si.search("cf", K, q_cf=torch.from_numpy(u), excl=eb, mask=mb)
+        res["hybrid/bits"] = si.search("hybrid", K, q_items=items, q_cf=torch.from_numpy(u), excl=eb, mask=mb)
         out_q.put((rank, {m: tuple(t.numpy() for t in v) for m, v in res.items()}))
     finally:
         dist.destroy_process_group()
@@ -98,7 +108,7 @@ def test_sharded_matches_unsharded(world):
     for rank in range(world):
         for mode, (sc, ids, cnt) in outs[rank].items():
             for b in range(B):
-                ri, rs = ref[mode][b]
+                ri, rs = ref[mode.split("/")[0]][b]
                 assert list(ids[b][: cnt[b]]) == list(ri), (rank, mode, b, ids[b], ri)
                 np.testing.assert_allclose(sc[b][: cnt[b]], rs, atol=1e-6)
     # identical on every rank
