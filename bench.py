@@ -54,20 +54,22 @@ def scan_kernel_info(dtype, width, batch):
     """(kernel, MFMA flops executed per algorithmic flop) of the scan that runs for an index
     of this dtype and padded width on a one-slab search.  An f32 index runs the exact
     re-rank path: a one-product bf16 MFMA scan (scan2 for up to 256 queries, scan4 above)
-    gives approximate scores within a proven bound, and rerank_kernel rescores the
-    candidates within it from the f32 rows (BB_NO_RR forces the older split-precision scan3,
-    six bf16 products per fp32 product).  A bf16 index runs scan2 / scan4 directly."""
-    if os.environ.get("BB_FORCE_TILED_GEMM"):
+    gives approximate scores within a proven bound and keeps bounded per-lane candidate lists,
+    and select_list_kernel rescores the candidates within the bound from the f32 rows
+    (BB_AB=1 BB_NO_RR forces the older split-precision scan3, six bf16 products per fp32
+    product).  A bf16 index runs scan2 / scan4 directly."""
+    ab = os.environ.get("BB_AB")   # A/B switches are honoured only with BB_AB set (csrc/common.h ab_env)
+    if ab and os.environ.get("BB_FORCE_TILED_GEMM"):
         return "gemm_nt_kernel", 1.0
     kern = "scan4_kernel" if batch > 256 else "scan2_kernel"
-    if dtype == "f32" and os.environ.get("BB_NO_RR") and not os.environ.get("BB_NO_SPLIT"):
+    if dtype == "f32" and ab and os.environ.get("BB_NO_RR") and not os.environ.get("BB_NO_SPLIT"):
         return f"scan3_kernel<{width * 2 // 16}> (bf16x6 split, f32 accumulate)", 6.0
-    if dtype == "f32" and os.environ.get("BB_NO_RR"):
+    if dtype == "f32" and ab and os.environ.get("BB_NO_RR"):
         return "scan2_kernel<float> (fp32 MFMA)", 1.0
     if dtype == "f32":
-        sel = "rerank_kernel" if batch <= 256 else "the one-wave select"
-        return (f"{kern}<uint16_t,{width * 2 // 16}> (one-product bf16 approximate scan, int16 score image; "
-                f"exact f32 re-rank of the candidates in {sel})"), 1.0
+        return (f"{kern}<uint16_t,{width * 2 // 16},list> (one-product bf16 approximate scan, bounded per-lane "
+                f"candidate lists in the epilogue, no score image; exact f32 re-rank of the candidates in "
+                f"select_list_kernel)"), 1.0
     return f"{kern}<uint16_t,{width * 2 // 16}> (bf16 MFMA)", 1.0
 
 
@@ -522,9 +524,10 @@ def main():
         flops = 2.0 * B * N_ITEMS * (DIM + r)
         alg_bytes = N_ITEMS * (DIM + r) * es + B * (r * 4 + 8) + B * TOPK * 12 + N_ITEMS // 8
         kname, mpf = scan_kernel_info(args.dtype, DIM, B)
-        if args.dtype == "f32" and not os.environ.get("BB_NO_RR") and os.environ.get("BB_DUAL", "1") != "0":
-            kname = ("scan4_dual_kernel<48,8> (content d=384 + CF r=50 one-product bf16 scans in one launch, "
-                     "int16 score image; exact f32 re-rank of the candidates in the one-wave select)")
+        ab = os.environ.get("BB_AB")
+        if args.dtype == "f32" and not (ab and os.environ.get("BB_NO_RR")) and not (ab and os.environ.get("BB_DUAL") == "0"):
+            kname = ("scan4_dual_kernel<48,8,list> (content d=384 + CF r=50 one-product bf16 scans in one launch, "
+                     "bounded per-lane candidate lists; exact f32 re-rank of the candidates in the list select)")
         kname = "scan launches of one hybrid step (content d=384 + CF r=50): " + kname
     else:
         flops = 2.0 * B * N_ITEMS * DIM

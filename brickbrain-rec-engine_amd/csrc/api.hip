@@ -118,6 +118,7 @@ struct bb_index {
   DevBuf rr_out, rr_cnt, rr_thr, rr_r0, rr_r0n;  // re-rank: select -> rerank hand-off
   // streaming top-K (large indexes): pilot lists, candidate regions, overflow flag
   DevBuf pilot, cand, cand_cnt, cand_pmax, ovf;
+  DevBuf pilot_top;  // kScanPilot scans: per lane the top-m half-tile maxima of the pilot rows
   DevBuf trace;        // BB_SELECT_TRACE probe stamps
   DevBuf rr_flags;     // one-wave re-rank select: rows left to the block select
   DevBuf list1, max1;  // two-level streaming: exact top-K_int (+ rank-0 key) of items [0, n1)
@@ -354,7 +355,7 @@ int bb_destroy(bb_index* x) {
                       &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
                       &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
                       &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
-                      &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists})
+                      &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists, &x->pilot_top})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
     if (x->has_last) (void)hipEventSynchronize(x->done);
@@ -637,7 +638,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   const int64_t rq = x->dtype == BF16 && B > kTileRows ? 2 * kTileRows : kTileRows;
   auto pad_rows = [&](int64_t b) { return round_up(b, b > kTileRows ? rq : kTileRows); };
   // BB_OPT_STREAM (or the BB_STREAM environment variable, for A/B runs) forces it off / on
-  static const int stream_env = getenv("BB_STREAM") ? atoi(getenv("BB_STREAM")) : -1;
+  static const int stream_env = ab_env("BB_STREAM") ? atoi(ab_env("BB_STREAM")) : -1;
   const int stream_sel = x->stream_opt >= 0 ? x->stream_opt : stream_env;
   // (the streaming epilogue lives in the query-resident scan kernels only)
   auto scan_ok = [&](int kp, bool planes) { return planes ? scan3_supported(128, kp) : gemm_uses_scan(x->dtype, 128, kp); };
@@ -673,7 +674,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   // exact re-rank path (f32 index, one slab): the one-product bf16 MFMA scan writes
   // approximate scores, the select rescores the candidates within their error bound from
   // the f32 rows.  BB_NO_RR (A/B runs) forces the split-precision scan instead.
-  static const bool no_rr = getenv("BB_NO_RR") != nullptr;
+  static const bool no_rr = ab_env("BB_NO_RR") != nullptr;
   const bool rr_c = !no_rr && !stream && n_slabs == 1 && need_content && x->items_bf.p;
   const bool rr_f = !no_rr && !stream && n_slabs == 1 && need_cf && x->cf_bf.p;
   // Bounded candidate lists (list_epi.h, select_list.hip) on the re-rank scans: no score
@@ -688,10 +689,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     const int tpc = (tiles + nch - 1) / nch;
     if (nch > 256) return false;
     np = (tpc + kListMaxPeriod - 1) / kListMaxPeriod;
-    while (2 * nch * np < 3 * K_int && 2 * nch * (np + 1) <= 1024 && np < tpc) ++np;
+    while (2 * nch * np < 3 * K_int && 2 * nch * (np + 1) <= kListMaxPerRow && np < tpc) ++np;
     G = (tpc + np - 1) / np;
     np = (tpc + G - 1) / G;
-    return G <= kListMaxPeriod && 2 * nch * np <= 1024;
+    return G <= kListMaxPeriod && 2 * nch * np <= kListMaxPerRow;
   };
 
   // stage host inputs
@@ -731,14 +732,14 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   // re-rank scans write an int16 score image (2 B per score: half the slab traffic of f32;
   // the quantum is folded into ε, common.h rr_quantum).  BB_S16=0 (A/B runs) keeps f32.
   // BB_S16: 0 off, 1 every re-rank scan, 2 only scan4 (query chunks > 256 rows)
-  static const int s16_env = getenv("BB_S16") ? atoi(getenv("BB_S16")) : 1;
+  static const int s16_env = ab_env("BB_S16") ? atoi(ab_env("BB_S16")) : 1;
   // The block select hands its candidates to a separate rerank_kernel launch; BB_RR_FUSED=1
   // makes the select kernel rescore them itself.  Measured on one box (r02zd, configs[1]):
   // fused serial p50 52.6 us vs 55.5 us split, but with three batches in flight split
   // 8.30 M q/s vs fused 7.66 M q/s — two shorter launches leave the CUs to the next batch's
   // scan sooner than one long one.  (The one-wave select of query chunks > 256 rows always
   // rescores in place.)
-  static const bool rr_split = !(getenv("BB_RR_FUSED") && atoi(getenv("BB_RR_FUSED")) == 1);
+  static const bool rr_split = !(ab_env("BB_RR_FUSED") && atoi(ab_env("BB_RR_FUSED")) == 1);
   if ((rr_c || rr_f) && rr_split &&
       ((rc = x->rr_out.ensure((size_t)Bc * kRrCap * 8)) || (rc = x->rr_cnt.ensure((size_t)Bc * 4)) ||
        (rc = x->rr_thr.ensure((size_t)Bc * 8)) || (rc = x->rr_r0.ensure((size_t)Bc * kRrR0Cap * 4)) ||
@@ -772,7 +773,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   // that list in the final select.  Expected appends per query drop from K_int·n/n0 to
   // K_int·(n1/n0 + n/n1), minimal at n1 = sqrt(n·n0): 16 -> 7 K_int at n0 = n/16 (1M rows),
   // 76 -> 16 K_int at n0 = n/76 (10M rows).  Appends are what the streaming scan pays for.
-  static const int refine_env = getenv("BB_STREAM_REFINE") ? atoi(getenv("BB_STREAM_REFINE")) : 1;
+  static const int refine_env = ab_env("BB_STREAM_REFINE") ? atoi(ab_env("BB_STREAM_REFINE")) : 1;
   // Auto (measured): from n >= 8·n0 on indexes of 500K+ rows with query chunks of 256+
   // (10M x 384, B=8192: 83 -> 71 ms; 1.25M: 12.4 -> 11.7 ms); on smaller indexes or batches
   // the extra candidate select costs more than the appends it saves (125K rows: 1.36 ->
@@ -832,7 +833,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     const bool gather_c = q->mode != BB_MODE_SEMANTIC && d_items;
     const float* rows_c = d_rows ? (const float*)((const char*)d_rows + (size_t)b0 * x->d * es_q) : nullptr;
     const float* rows_f = d_cf ? (const float*)((const char*)d_cf + (size_t)b0 * x->r * es_cf) : nullptr;
-    static const bool no_fuse = getenv("BB_NO_FUSE_PREP") != nullptr;
+    static const bool no_fuse = ab_env("BB_NO_FUSE_PREP") != nullptr;
     const bool fuse_c = !no_fuse && need_content && scan_c &&
                         (gather_c || (x->dtype == F32 && q->q_dtype == F32 && x->d % 4 == 0 && rows_c &&
                                       ((uintptr_t)rows_c & 15) == 0));
@@ -843,7 +844,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // chunk-0 workgroups write the f32 rows + ε the select needs — no prep launch
     // (opt-in, BB_RR_FUSE_PREP: the per-lane query loads of the prologue cost more than the
     // prep launch they replace — r02s: scan 20.8 -> 33.8 us vs prep 7.6 us at configs[1])
-    static const bool rr_fuse_prep = getenv("BB_RR_FUSE_PREP") != nullptr;
+    static const bool rr_fuse_prep = ab_env("BB_RR_FUSE_PREP") != nullptr;
     const bool rrfuse_c = rr_fuse_prep && !no_fuse && rr_c && !scan4_used(BF16, bpad) &&
                           (gather_c || (q->q_dtype == F32 && x->d % 4 == 0 && rows_c && ((uintptr_t)rows_c & 15) == 0));
     const bool rrfuse_f = rr_fuse_prep && !no_fuse && rr_f && !scan4_used(BF16, bpad) && q->q_cf_dtype == F32 && x->r % 4 == 0 &&
@@ -916,6 +917,14 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       pa.src_ld = x->r;
       pa.normalize = 0;
     }
+    // the bf16 operand of a scan4 launch goes out in its lane order (scan4_q_offset):
+    // coalesced prologue loads (at 1,024 x 384 the row-major loads took ~8 of a 23 us scan)
+    const bool perm_c = prep_c && !s3_c && scan4_used(BF16, bpad) &&
+                        (rr_c ? gemm_uses_scan(BF16, bpad, x->Dpad_b) : x->dtype == BF16 && scan_c);
+    const bool perm_f = prep_f && !s3_f && scan4_used(BF16, bpad) &&
+                        (rr_f ? gemm_uses_scan(BF16, bpad, x->Rpad_b) : x->dtype == BF16 && scan_f);
+    pa_c.q_perm = perm_c ? 1 : 0;
+    pa_f.q_perm = perm_f ? 1 : 0;
     if (prep_c && prep_f) {
       if ((rc = timed(x, K_PREP, s, [&] { return launch_prep2(pa_c, pa_f, s); }))) return rc;
     } else if (prep_c || prep_f) {
@@ -928,8 +937,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // maxima / flag rows.  Measured (r02za, configs[2]): serial p50 222 -> 173 us (scan 86 ->
     // 77 us, select 116 -> 62 us per step); with three batches in flight 6.6 -> 6.3 M q/s.
     // BB_DUAL=0 (A/B runs) keeps one launch per side.
-    static const bool dual_env = !(getenv("BB_DUAL") && atoi(getenv("BB_DUAL")) == 0);
-    static const int sel_wave_env0 = getenv("BB_SELECT_WAVE") ? atoi(getenv("BB_SELECT_WAVE")) : -1;
+    static const bool dual_env = !(ab_env("BB_DUAL") && atoi(ab_env("BB_DUAL")) == 0);
+    static const int sel_wave_env0 = ab_env("BB_SELECT_WAVE") ? atoi(ab_env("BB_SELECT_WAVE")) : -1;
     const bool dual = dual_env && q->mode == BB_MODE_HYBRID && sides == 2 && ((s16_c && s16_f) || (list_c && list_f)) &&
                       !stream &&
                       n_slabs == 1 && scan4_used(BF16, bpad) && scan4_dual_supported((int)x->Dpad_b / 8, (int)x->Rpad_b / 8) &&
@@ -941,6 +950,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     for (int side = 0; side < sides; ++side) {
       const bool cf_side = (q->mode == BB_MODE_CF) || (q->mode == BB_MODE_HYBRID && side == 1);
       const bool side_drop = drop && side == 0;
+      bool pilot_topm = false;  // this side's pilot left one bound key per row (thr_ld 1)
       // stream: pass 0 = the pilot slab [0, n0) -> pilot lists, pass 1 = the streaming scan
       // (A: [0, n1)), pass 2 with the two-level bound (B: [n1, n))
       const int64_t n_pass = stream ? (refine ? 3 : 2) : n_slabs;
@@ -954,6 +964,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         const int ncols_pad = (int)round_up(ncols, kTileRows);
         GemmArgs ga{};
         ga.Q = cf_side ? x->qcf.p : x->qn.p;
+        ga.q_perm = (cf_side ? perm_f : perm_c) ? 1 : 0;
         ga.ldq = cf_side ? x->Rpad : x->Dpad;
         ga.X = (const char*)(cf_side ? x->cf.p : x->items.p) + (size_t)c0 * ga.ldq * es;
         ga.ldx = ga.ldq;
@@ -982,7 +993,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         if (spass) {
           stream_geom(bpad, sp, regions, cand_cap);
           ga.thr_keys = (const uint64_t*)(sp == 0 ? x->pilot.p : x->list1.p);
-          ga.thr_ld = K_int;
+          ga.thr_ld = sp == 0 && pilot_topm ? 1 : K_int;
           ga.cand = (uint64_t*)x->cand.p;
           ga.cand_cnt = (uint32_t*)x->cand_cnt.p;
           ga.cand_pmax = side_drop ? (uint64_t*)x->cand_pmax.p : nullptr;
@@ -1053,8 +1064,31 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           ga.ldx = 3 * w;
           ga.ldq = 3 * w;
           if ((rc = timed(x, K_GEMM, s, [&] { return launch_scan3(ga, s); }))) return rc;
-        } else if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(x->dtype, ga, s); }))) {
-          return rc;
+        } else {
+          // Streaming pilot on scan4 (bf16 index): no B×n0 score image and no pilot select —
+          // the scan keeps each lane's top-m eligible half-tile maxima and pilot_bound_kernel
+          // turns them into one bound key per row (configs[3]: the image was 1.0 GB written
+          // plus 0.7 GB of scattered maxima stores per batch)
+          const int tiles_p = ncols_pad / 32;
+          bool use_top = pilot && x->dtype == BF16 && scan4_used(BF16, bpad) && gemm_uses_scan(BF16, bpad, ga.Kpad);
+          const int nch_p = use_top ? scan_chunks(BF16, bpad, tiles_p, false) : 0;
+          const int m_p = use_top ? scan4_pilot_m(ga.Kpad) : 0;
+          use_top = use_top && 2 * nch_p * m_p <= 16 * 256;
+          if (pilot) pilot_topm = use_top;
+          if (use_top) {
+            if ((rc = x->pilot_top.ensure((size_t)nch_p * (bpad / 32) * 64 * m_p * 4))) return rc;
+            ga.pilot_top = (uint32_t*)x->pilot_top.p;
+            ga.pilot_m = m_p;
+          }
+          if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(x->dtype, ga, s); }))) return rc;
+          if (use_top) {
+            if ((rc = timed(x, K_SELECT, s, [&] {
+                   return launch_pilot_bound((const uint32_t*)x->pilot_top.p, nch_p, m_p, bpad / 32, K_int, bc,
+                                             (uint64_t*)x->pilot.p, s);
+                 })))
+              return rc;
+            continue;  // no pilot select
+          }
         }
         if (spass) {
           // candidate select: exact top-K_int of the appended candidates of each query
@@ -1144,7 +1178,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
             continue;
           }
           const bool both = q->mode == BB_MODE_HYBRID && side == 1 && list_c;
-          static const bool ls_trace = getenv("BB_SELECT_TRACE") != nullptr;
+          static const bool ls_trace = ab_env("BB_SELECT_TRACE") != nullptr;
           if (ls_trace) {  // probe runs: phase stamps of side 0's rows (16 words per row)
             if ((rc = x->trace.ensure((size_t)bc * 16 * 8))) return rc;
             BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 128, s));
@@ -1200,7 +1234,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         }
         // BB_SELECT_TRACE (probe runs): per-phase s_memrealtime stamps of every query row,
         // averaged over the rows and printed to stderr
-        static const bool sel_trace = getenv("BB_SELECT_TRACE") != nullptr;
+        static const bool sel_trace = ab_env("BB_SELECT_TRACE") != nullptr;
         if (sel_trace) {
           if ((rc = x->trace.ensure((size_t)bc * 8 * 8))) return rc;
           BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 64, s));
@@ -1211,7 +1245,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         // others).  Measured (r02y): B=1024 10.2 -> 10.5 M q/s, B=4096 10.9 -> 11.9 M q/s in
         // flight; at B <= 256 the block select's four waves per query win on latency (19 vs
         // 34 us per query).  BB_SELECT_WAVE=0/1 (A/B runs) forces it off / on.
-        static const int sel_wave_env = getenv("BB_SELECT_WAVE") ? atoi(getenv("BB_SELECT_WAVE")) : -1;
+        static const int sel_wave_env = ab_env("BB_SELECT_WAVE") ? atoi(ab_env("BB_SELECT_WAVE")) : -1;
         const bool sel_wave = rr_side && !sa.carry_in && ncols <= 32768 && K_int <= 256 &&
                               (!sa.out_scores || q->k <= 256) &&
                               (sel_wave_env == 1 || (sel_wave_env != 0 && bc > 256));
@@ -1316,7 +1350,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     fa.ids = o_id + (size_t)b0 * q->k;
     fa.counts = o_cnt ? o_cnt + b0 : nullptr;
     fa.n_rows = bc;
-    static const bool fin_trace = getenv("BB_SELECT_TRACE") != nullptr;
+    static const bool fin_trace = ab_env("BB_SELECT_TRACE") != nullptr;
     if (fin_trace) {
       if ((rc = x->trace.ensure((size_t)bc * 8 * 8))) return rc;
       BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 64, s));
@@ -1349,7 +1383,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // the caller reruns the search on the exact slab path
     BB_HIP(hipMemcpyAsync(x->ovf_host, x->ovf.p, 4, hipMemcpyDeviceToHost, s));
     BB_HIP(hipStreamSynchronize(s));
-    if (*x->ovf_host && getenv("BB_STREAM_DEBUG")) {
+    if (*x->ovf_host && ab_env("BB_STREAM_DEBUG")) {
       int rg, cap;
       const int bpl = (int)pad_rows(B - (B - 1) / Bc * Bc);
       stream_geom(bpl, refine ? 1 : 0, rg, cap);

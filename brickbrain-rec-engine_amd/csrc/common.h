@@ -1,9 +1,18 @@
 // common.h — shared device/host definitions of libbrickrec (gfx950 / CDNA4 only).
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace bb {
+
+// A/B and probe switches (BB_NO_RR, BB_S16, BB_DUAL, BB_SELECT_TRACE, ...): read only when
+// BB_AB is set in the environment, so a production process is immune to stray variables;
+// tools/gpu_run.sh sets it for its A/B runs.  Defaults are the measured best.
+inline const char* ab_env(const char* name) {
+  static const bool on = std::getenv("BB_AB") != nullptr;
+  return on ? std::getenv(name) : nullptr;
+}
 
 // ---- item ordering keys ------------------------------------------------------------------
 // A candidate is one u64: high word = order-preserving image of the fp32 score, low word =
@@ -97,10 +106,25 @@ struct GemmArgs {
   uint32_t* lists;          // uint4 at list_slot(chunk, period, l_np, Mpad/32, q >> 5, lane)
   uint32_t* r0lists;        // uint2 at list_slot(chunk, 0, 1, Mpad/32, q >> 5, lane), or null
   int32_t l_period, l_np;
+  int32_t q_perm;           // scan4: Q holds the prepped operand in lane order (scan4_q_offset)
+  // streaming pilot (scan ABL kScanPilot): no score image; per lane the top pilot_m of its
+  // eligible half-tile maxima over the item chunk, u32 order images at
+  // ((chunk·(Mpad/32) + q/32)·64 + lane)·pilot_m (pilot_bound_kernel turns them into bounds)
+  uint32_t* pilot_top;
+  int32_t pilot_m;
 };
+// The scan4 query operand in lane order (PrepArgs / GemmArgs.q_perm): 16-B chunk c = 2u + h of
+// query row q (Kpad/8 chunks per row, U = Kpad/16 u-steps) sits where lane (r, h) of wave w of
+// group g loads query register j = b·U + u — one contiguous 1-KiB wave load per register,
+// where row-major rows made every prologue load touch 32 lines for 16 B each.
+__host__ __device__ inline size_t scan4_q_offset(int q, int c, int U) {  // in 16-B units
+  const int g = q >> 8, w = (q >> 6) & 3, b = (q >> 5) & 1, r = q & 31, u = c >> 1, h = c & 1;
+  return ((size_t)(g * 4 + w) * (2 * U) + b * U + u) * 64 + h * 32 + r;
+}
 constexpr int kScanStream = 512;  // scan ABL bit: streaming top-K epilogue
 constexpr int kScanS16 = 4096;    // scan ABL bit: int16 score image (GemmArgs.s_h)
 constexpr int kScanList = 8192;   // scan ABL bit: bounded candidate lists (GemmArgs.lists)
+constexpr int kScanPilot = 16384; // scan ABL bit: streaming pilot, top-m half-tile maxima (GemmArgs.pilot_top)
 
 // Quantum h of the int16 score image of one query and the widened bound of its decoded
 // scores.  |approximate score| <= |q̃|·Ñ_x·(1+γ) <= 16384·h, so no code saturates; the
@@ -290,6 +314,7 @@ struct PrepArgs {
   float* eps_out;           // [Bpad]
   const float* istats;      // [3]: max |x̃−x|, max |x|, max |x̃| over the item rows
   float* h_out;             // [Bpad] int16 score-image quantum (rr_quantum; eps_out widened), or null
+  int32_t q_perm;           // 1: the bf16 operand in scan4 lane order (scan4_q_offset), not row-major
 };
 
 struct MaskArgs {
@@ -311,6 +336,7 @@ bool scan4_used(int dtype, int Mpad);                // bf16 scan with 64 querie
 // item chunks (candidate regions / 2 per query) of the scan launch for these shapes
 int scan_chunks(int dtype, int Mpad, int tiles, bool split);
 bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s);  // scan4_used(BF16, a.Mpad) shapes
+int scan4_pilot_m(int kpad);  // GemmArgs.pilot_m of a kScanPilot scan4 launch
 bool scan4_dual_supported(int ku0, int ku1);
 hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s);  // hybrid, int16 image
 hipError_t launch_scan3(const GemmArgs& a, hipStream_t s);  // X = item planes, Q = q3f image
@@ -332,6 +358,11 @@ hipError_t launch_select_rr_wave_dual(const SelectArgs& a0, const SelectArgs& a1
 hipError_t launch_select_list(const SelectArgs& a0, const SelectArgs* a1, int B, hipStream_t s);
 hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
+// streaming bound of each query row from a kScanPilot scan: the K-th largest of its
+// 2·n_chunks·m half-tile maxima (K distinct half tiles, so K distinct items reach it), as
+// a key (ord << 32) in thr_out[row]; 0 (take every eligible item) when fewer than K exist
+hipError_t launch_pilot_bound(const uint32_t* top, int n_chunks, int m, int nb, int K, int B, uint64_t* thr_out,
+                              hipStream_t s);
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s);
 hipError_t launch_prep2(const PrepArgs& a0, const PrepArgs& a1, hipStream_t s);
 hipError_t launch_mask(const MaskArgs& a, hipStream_t s);

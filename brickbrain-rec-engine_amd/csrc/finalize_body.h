@@ -1,0 +1,193 @@
+// finalize_body.h — the single-shard finalize of one query row (finalize1): rank-0 drop,
+// truncation and the hybrid union blend of _combine_recommendations
+// (recommendation_system.py:789-843) over two sorted, unique side lists, templated on the
+// list capacity; finalize1_kernel runs it on lists read from global memory.  (A hybrid list
+// select running both sides and this blend in one workgroup per row measured slower than
+// two side workgroups + finalize1: 100.7 vs 50.3 + 19.4 us at configs[2])
+#pragma once
+#include "common.h"
+
+namespace bb {
+
+constexpr int kFinThreads = 256;
+
+__device__ __forceinline__ uint64_t ord64_of(double d) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+// Single-shard fast path (P == 1: each side's key list is already sorted and unique): no
+// serial list walk and no sort network.  Each side's list is sliced in parallel (rank-0
+// drop = skip the head when it is the unmasked arg-max maxk), the union blend looks each id
+// up in the other list, and every blended entry finds its output position as its rank
+// under (h desc, id asc) — O(n²) independent comparisons, n <= 2·k_side, no barriers inside.
+// k0 / k1: the side lists (a.K_int keys each, generic pointers: global or LDS).
+template <int KC>
+__device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, const uint64_t* k0, const uint64_t* k1,
+                                               uint64_t maxk) {
+  __shared__ uint64_t lst[2][KC];
+  __shared__ double eh[2 * KC];
+  __shared__ uint64_t ek[2 * KC];  // order image of eh (the legacy kernel's sort key)
+  __shared__ uint32_t eg[2 * KC];
+  __shared__ __attribute__((aligned(16))) uint32_t ehi[2 * KC];  // order image of (float)eh
+  __shared__ int nnz[2], n_ent;
+  const int tid = threadIdx.x;
+  auto stamp = [&](int slot) {  // probe-only phase timeline (s_memrealtime, 100 MHz)
+    if (a.trace && tid == 0) a.trace[q * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  if (tid < 2) nnz[tid] = 0;
+  if (tid == 0) n_ent = 0;
+  __syncthreads();
+  int cnt_local[2] = {0, 0};
+  for (int side = 0; side < a.sides; ++side)
+    for (int i = tid; i < a.K_int; i += kFinThreads) {
+      const uint64_t key = (side ? k1 : k0)[i];
+      lst[side][i] = key;
+      cnt_local[side] += key != 0ull;
+    }
+  for (int side = 0; side < a.sides; ++side)
+    if (cnt_local[side]) atomicAdd(&nnz[side], cnt_local[side]);
+  __syncthreads();
+  stamp(1);
+  int start[2] = {0, 0}, c[2] = {0, 0};
+  for (int side = 0; side < a.sides; ++side) {
+    const uint64_t head = lst[side][0];
+    if (side == 0 && a.drop_rank0 && maxk && head && head == maxk) start[side] = 1;
+    const int target = a.hybrid ? a.k_side : a.k;
+    const int avail = nnz[side] - start[side];
+    c[side] = avail < target ? (avail > 0 ? avail : 0) : target;
+  }
+  float* sc = a.scores + (size_t)q * a.k;
+  int64_t* id = a.ids + (size_t)q * a.k;
+  if (!a.hybrid || c[0] == 0 || c[1] == 0) {
+    const int side = (!a.hybrid || c[0] > 0) ? 0 : 1;
+    const int n = c[side] < a.k ? c[side] : a.k;
+    for (int i = tid; i < a.k; i += kFinThreads) {
+      if (i < n) {
+        const uint64_t key = lst[side][start[side] + i];
+        sc[i] = float_of_ord(ordk_of(key));
+        id[i] = (int64_t)gid_of(key);
+      } else {
+        sc[i] = 0.f;
+        id[i] = -1;
+      }
+    }
+    if (a.counts && tid == 0) a.counts[q] = n;
+    return;
+  }
+  // union blend (recommendation_system.py:789-843): content entries, then CF-only entries.
+  // CF ids go into an LDS hash table (open addressing, 2·KC slots: load <= 1/2); each
+  // content entry looks its id up there and marks the CF entry it consumed.
+  const uint64_t* L0 = lst[0] + start[0];
+  const uint64_t* L1 = lst[1] + start[1];
+  constexpr int kTab = 2 * KC;
+  __shared__ uint32_t tab_g[kTab];   // gid + 1 (0 = empty)
+  __shared__ uint16_t tab_j[kTab];
+  __shared__ uint8_t used[KC];
+  for (int i = tid; i < kTab; i += kFinThreads) tab_g[i] = 0u;
+  for (int j = tid; j < c[1]; j += kFinThreads) used[j] = 0;
+  __syncthreads();
+  stamp(2);
+  auto slot0 = [](uint32_t g) { return (int)((g * 2654435761u) >> 22) & (kTab - 1); };
+  for (int j = tid; j < c[1]; j += kFinThreads) {
+    const uint32_t g = gid_of(L1[j]);
+    for (int sl = slot0(g);; sl = (sl + 1) & (kTab - 1))
+      if (atomicCAS(&tab_g[sl], 0u, g + 1u) == 0u) {
+        tab_j[sl] = (uint16_t)j;
+        break;
+      }
+  }
+  __syncthreads();
+  for (int i = tid; i < c[0]; i += kFinThreads) {
+    const uint32_t g = gid_of(L0[i]);
+    int hit = -1;
+    for (int sl = slot0(g);; sl = (sl + 1) & (kTab - 1)) {
+      const uint32_t t = tab_g[sl];
+      if (t == 0u) break;
+      if (t == g + 1u) {
+        hit = tab_j[sl];
+        break;
+      }
+    }
+    if (hit >= 0) used[hit] = 1;
+    const double cs = (double)float_of_ord(ordk_of(L0[i]));
+    const double fs = hit >= 0 ? (double)float_of_ord(ordk_of(L1[hit])) : 0.0;
+    eh[i] = a.w_content * cs + a.w_cf * fs;
+    ek[i] = ord64_of(eh[i]);
+    ehi[i] = ord_of((float)eh[i]);
+    eg[i] = g;
+  }
+  __syncthreads();
+  stamp(3);
+  for (int j = tid; j < c[1]; j += kFinThreads) {
+    const uint32_t g = gid_of(L1[j]);
+    if (!used[j]) {
+      const int pos = c[0] + atomicAdd(&n_ent, 1);
+      eh[pos] = a.w_content * 0.0 + a.w_cf * (double)float_of_ord(ordk_of(L1[j]));
+      ek[pos] = ord64_of(eh[pos]);
+      ehi[pos] = ord_of((float)eh[pos]);
+      eg[pos] = g;
+    }
+  }
+  __syncthreads();
+  stamp(4);
+  const int ne = c[0] + n_ent;
+  const int n = ne < a.k ? ne : a.k;
+  // output position = rank under (h desc, id asc).  Counted on the order image of the f32
+  // rounding of h first (monotonic in h; 16 entries per round from four ds_read_b128
+  // broadcasts, two 32-bit compares each): entries above are better, below worse.  Only
+  // entries sharing that image with others (ties and near-ties, rare) take the full (h, id)
+  // comparison among them, batched the same way.  The
+  // full 96-bit count for every pair, with 32 LDS reads per round, took 9.5 us of the 21 us
+  // kernel at configs[2] (r02u trace).
+  for (int e = tid; e < ne; e += kFinThreads) {
+    const uint64_t hk = ek[e];
+    const uint32_t g = eg[e], hh = ehi[e];
+    int gt = 0, ge = 0, f = 0;
+    for (; f + 16 <= ne; f += 16) {
+      uint32_t kk[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *(uint4*)(kk + 4 * j) = *(const uint4*)(ehi + f + 4 * j);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        gt += kk[j] > hh;
+        ge += kk[j] >= hh;
+      }
+    }
+    for (; f < ne; ++f) {
+      gt += ehi[f] > hh;
+      ge += ehi[f] >= hh;
+    }
+    int rank = gt;
+    if (ge - gt > 1) {
+      for (f = 0; f + 16 <= ne; f += 16) {
+        uint32_t kk[16], gg[16];
+        uint64_t hv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          kk[j] = ehi[f + j];
+          hv[j] = ek[f + j];
+          gg[j] = eg[f + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) rank += kk[j] == hh && ((hv[j] > hk) || (hv[j] == hk && gg[j] < g));
+      }
+      for (; f < ne; ++f) rank += ehi[f] == hh && ((ek[f] > hk) || (ek[f] == hk && eg[f] < g));
+    }
+    if (rank < a.k) {
+      sc[rank] = (float)eh[e];
+      id[rank] = (int64_t)g;
+    }
+  }
+  for (int i = n + tid; i < a.k; i += kFinThreads) {
+    sc[i] = 0.f;
+    id[i] = -1;
+  }
+  if (a.counts && tid == 0) a.counts[q] = n;
+  __syncthreads();
+  stamp(5);
+}
+
+
+}  // namespace bb

@@ -100,7 +100,7 @@ bool scan_supported(int dtype, int Kpad) {
 bool scan3_supported(int Mpad, int Kpad) {
   const int kp = Kpad * 2 / 16;
   return Mpad % (kScanWaves * 32) == 0 && Kpad % 8 == 0 && kp % 8 == 0 && kp >= 8 && kp <= kScan3MaxKP &&
-         !getenv("BB_NO_SPLIT");
+         !ab_env("BB_NO_SPLIT");
 }
 
 template <int KP>
@@ -132,7 +132,7 @@ hipError_t launch_scan3(const GemmArgs& a, hipStream_t s) {
 }
 
 bool gemm_uses_scan(int dtype, int Mpad, int Kpad) {
-  return Mpad % (kScanWaves * 32) == 0 && scan_supported(dtype, Kpad) && !getenv("BB_FORCE_TILED_GEMM");
+  return Mpad % (kScanWaves * 32) == 0 && scan_supported(dtype, Kpad) && !ab_env("BB_FORCE_TILED_GEMM");
 }
 
 hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
@@ -149,6 +149,14 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   // at most kListMaxPeriod tiles covering every chunk
   if (a.lists && (!a.s_h || a.q_istats || a.cand || a.l_period <= 0 || a.l_period > kListMaxPeriod || a.l_np <= 0 ||
                   (int64_t)a.l_period * a.l_np * scan_chunks(BF16, a.Mpad, a.Ncols / 32, false) < a.Ncols / 32))
+    return hipErrorInvalidValue;
+  // the streaming pilot's top-m maxima: scan4 (bf16), slab mode, no other epilogue output
+  if (a.pilot_top && (dtype != BF16 || !scan4_used(BF16, a.Mpad) || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.cand ||
+                      a.lists || a.s_h || a.pilot_m != scan4_pilot_m(a.Kpad)))
+    return hipErrorInvalidValue;
+  // the lane-order query operand is scan4's (prepped rows, no fused query prologue)
+  if (a.q_perm && (dtype != BF16 || !scan4_used(BF16, a.Mpad) || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.q_ids ||
+                   a.q_src))
     return hipErrorInvalidValue;
   if (gemm_uses_scan(dtype, a.Mpad, a.Kpad)) {
     if (dtype == BF16 ? launch_scan<uint16_t>(a, s) : launch_scan<float>(a, s)) return hipGetLastError();

@@ -73,6 +73,7 @@ __host__ __device__ inline void list_unpack5(uint4 v, uint32_t c[5], uint32_t p[
   p[4] = v.w & 0x7Fu;
 }
 constexpr int kListMaxPeriod = 8;  // tiles per period: 7-bit positions
+constexpr int kListMaxPerRow = 512;  // lists per query row (2·chunks·periods) the list select takes
 
 struct ListTop2 {
   uint32_t k0 = 0, k1 = 0;

@@ -1,6 +1,7 @@
 // misc.hip — query preparation, cross-slab/shard finalize (rank-0 drop, hybrid
 // union-blend), hard-constraint predicate masks and item-row conversion (gfx950).
 #include "common.h"
+#include "finalize_body.h"
 
 #include <cstdlib>
 
@@ -211,6 +212,8 @@ __device__ __forceinline__ void store_q(const PrepArgs& a, int row, int i, float
     o[0] = h;
     o[plane] = m;
     o[2 * plane] = l;
+  } else if (a.q_perm) {  // bf16 operand in scan4 lane order
+    ((uint16_t*)a.out)[scan4_q_offset(row, i >> 3, a.Dpad >> 4) * 8 + (i & 7)] = to_bf16(v);
   } else {
     store_elem(a.out, a.out_dtype, (size_t)row * a.Dpad + i, v);
   }
@@ -351,13 +354,7 @@ hipError_t launch_prep2(const PrepArgs& a0, const PrepArgs& a1, hipStream_t s) {
 // floats), sort by (h desc, id asc), top k.  One side empty -> the other side's top k
 // with its raw scores (:659-662).  One workgroup per query.
 // ---------------------------------------------------------------------------------------
-constexpr int kFinThreads = 256;
 constexpr int kFinMerge = 4096;  // P * K_int capacity
-
-__device__ __forceinline__ uint64_t ord64_of(double d) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, d);
-  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
-}
 
 template <typename T, typename Better>
 __device__ void bitonic_desc(T* v, int P, Better better) {
@@ -385,174 +382,10 @@ struct Blend {
   double hv;
 };
 
-// Single-shard fast path (P == 1: each side's key list is already sorted and unique): no
-// serial list walk and no sort network.  Each side's list is sliced in parallel (rank-0
-// drop = skip the head when it is the unmasked arg-max), the union blend looks each id up
-// in the other list, and every blended entry finds its output position as its rank under
-// (h desc, id asc) — O(n²) independent comparisons, n <= 2·k_side, no barriers inside.
 __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) {
-  __shared__ uint64_t lst[2][kMaxKInt];
-  __shared__ double eh[2 * kMaxKInt];
-  __shared__ uint64_t ek[2 * kMaxKInt];  // order image of eh (the legacy kernel's sort key)
-  __shared__ uint32_t eg[2 * kMaxKInt];
-  __shared__ __attribute__((aligned(16))) uint32_t ehi[2 * kMaxKInt];  // order image of (float)eh
-  __shared__ int nnz[2], n_ent;
-  const int q = blockIdx.x, tid = threadIdx.x;
-  auto stamp = [&](int slot) {  // probe-only phase timeline (s_memrealtime, 100 MHz)
-    if (a.trace && tid == 0) a.trace[q * 8 + slot] = __builtin_amdgcn_s_memrealtime();
-  };
-  stamp(0);
-  if (tid < 2) nnz[tid] = 0;
-  if (tid == 0) n_ent = 0;
-  __syncthreads();
-  int cnt_local[2] = {0, 0};
-  for (int side = 0; side < a.sides; ++side)
-    for (int i = tid; i < a.K_int; i += kFinThreads) {
-      const uint64_t key = a.keys[((size_t)side * a.B + q) * a.K_int + i];
-      lst[side][i] = key;
-      cnt_local[side] += key != 0ull;
-    }
-  for (int side = 0; side < a.sides; ++side)
-    if (cnt_local[side]) atomicAdd(&nnz[side], cnt_local[side]);
-  __syncthreads();
-  stamp(1);
-  int start[2] = {0, 0}, c[2] = {0, 0};
-  for (int side = 0; side < a.sides; ++side) {
-    const uint64_t head = lst[side][0];
-    if (side == 0 && a.drop_rank0 && a.max_keys && head && head == a.max_keys[q]) start[side] = 1;
-    const int target = a.hybrid ? a.k_side : a.k;
-    const int avail = nnz[side] - start[side];
-    c[side] = avail < target ? (avail > 0 ? avail : 0) : target;
-  }
-  float* sc = a.scores + (size_t)q * a.k;
-  int64_t* id = a.ids + (size_t)q * a.k;
-  if (!a.hybrid || c[0] == 0 || c[1] == 0) {
-    const int side = (!a.hybrid || c[0] > 0) ? 0 : 1;
-    const int n = c[side] < a.k ? c[side] : a.k;
-    for (int i = tid; i < a.k; i += kFinThreads) {
-      if (i < n) {
-        const uint64_t key = lst[side][start[side] + i];
-        sc[i] = float_of_ord(ordk_of(key));
-        id[i] = (int64_t)gid_of(key);
-      } else {
-        sc[i] = 0.f;
-        id[i] = -1;
-      }
-    }
-    if (a.counts && tid == 0) a.counts[q] = n;
-    return;
-  }
-  // union blend (recommendation_system.py:789-843): content entries, then CF-only entries.
-  // CF ids go into an LDS hash table (open addressing, 2·kMaxKInt slots: load <= 1/2); each
-  // content entry looks its id up there and marks the CF entry it consumed.
-  const uint64_t* L0 = lst[0] + start[0];
-  const uint64_t* L1 = lst[1] + start[1];
-  constexpr int kTab = 2 * kMaxKInt;
-  __shared__ uint32_t tab_g[kTab];   // gid + 1 (0 = empty)
-  __shared__ uint16_t tab_j[kTab];
-  __shared__ uint8_t used[kMaxKInt];
-  for (int i = tid; i < kTab; i += kFinThreads) tab_g[i] = 0u;
-  for (int j = tid; j < c[1]; j += kFinThreads) used[j] = 0;
-  __syncthreads();
-  stamp(2);
-  auto slot0 = [](uint32_t g) { return (int)((g * 2654435761u) >> 22) & (kTab - 1); };
-  for (int j = tid; j < c[1]; j += kFinThreads) {
-    const uint32_t g = gid_of(L1[j]);
-    for (int sl = slot0(g);; sl = (sl + 1) & (kTab - 1))
-      if (atomicCAS(&tab_g[sl], 0u, g + 1u) == 0u) {
-        tab_j[sl] = (uint16_t)j;
-        break;
-      }
-  }
-  __syncthreads();
-  for (int i = tid; i < c[0]; i += kFinThreads) {
-    const uint32_t g = gid_of(L0[i]);
-    int hit = -1;
-    for (int sl = slot0(g);; sl = (sl + 1) & (kTab - 1)) {
-      const uint32_t t = tab_g[sl];
-      if (t == 0u) break;
-      if (t == g + 1u) {
-        hit = tab_j[sl];
-        break;
-      }
-    }
-    if (hit >= 0) used[hit] = 1;
-    const double cs = (double)float_of_ord(ordk_of(L0[i]));
-    const double fs = hit >= 0 ? (double)float_of_ord(ordk_of(L1[hit])) : 0.0;
-    eh[i] = a.w_content * cs + a.w_cf * fs;
-    ek[i] = ord64_of(eh[i]);
-    ehi[i] = ord_of((float)eh[i]);
-    eg[i] = g;
-  }
-  __syncthreads();
-  stamp(3);
-  for (int j = tid; j < c[1]; j += kFinThreads) {
-    const uint32_t g = gid_of(L1[j]);
-    if (!used[j]) {
-      const int pos = c[0] + atomicAdd(&n_ent, 1);
-      eh[pos] = a.w_content * 0.0 + a.w_cf * (double)float_of_ord(ordk_of(L1[j]));
-      ek[pos] = ord64_of(eh[pos]);
-      ehi[pos] = ord_of((float)eh[pos]);
-      eg[pos] = g;
-    }
-  }
-  __syncthreads();
-  stamp(4);
-  const int ne = c[0] + n_ent;
-  const int n = ne < a.k ? ne : a.k;
-  // output position = rank under (h desc, id asc).  Counted on the order image of the f32
-  // rounding of h first (monotonic in h; 16 entries per round from four ds_read_b128
-  // broadcasts, two 32-bit compares each): entries above are better, below worse.  Only
-  // entries sharing that image with others (ties and near-ties, rare) take the full (h, id)
-  // comparison among them, batched the same way.  The
-  // full 96-bit count for every pair, with 32 LDS reads per round, took 9.5 us of the 21 us
-  // kernel at configs[2] (r02u trace).
-  for (int e = tid; e < ne; e += kFinThreads) {
-    const uint64_t hk = ek[e];
-    const uint32_t g = eg[e], hh = ehi[e];
-    int gt = 0, ge = 0, f = 0;
-    for (; f + 16 <= ne; f += 16) {
-      uint32_t kk[16];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) *(uint4*)(kk + 4 * j) = *(const uint4*)(ehi + f + 4 * j);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        gt += kk[j] > hh;
-        ge += kk[j] >= hh;
-      }
-    }
-    for (; f < ne; ++f) {
-      gt += ehi[f] > hh;
-      ge += ehi[f] >= hh;
-    }
-    int rank = gt;
-    if (ge - gt > 1) {
-      for (f = 0; f + 16 <= ne; f += 16) {
-        uint32_t kk[16], gg[16];
-        uint64_t hv[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          kk[j] = ehi[f + j];
-          hv[j] = ek[f + j];
-          gg[j] = eg[f + j];
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) rank += kk[j] == hh && ((hv[j] > hk) || (hv[j] == hk && gg[j] < g));
-      }
-      for (; f < ne; ++f) rank += ehi[f] == hh && ((ek[f] > hk) || (ek[f] == hk && eg[f] < g));
-    }
-    if (rank < a.k) {
-      sc[rank] = (float)eh[e];
-      id[rank] = (int64_t)g;
-    }
-  }
-  for (int i = n + tid; i < a.k; i += kFinThreads) {
-    sc[i] = 0.f;
-    id[i] = -1;
-  }
-  if (a.counts && tid == 0) a.counts[q] = n;
-  __syncthreads();
-  stamp(5);
+  const int q = blockIdx.x;
+  finalize1_body<kMaxKInt>(a, q, a.keys + (size_t)q * a.K_int, a.keys + ((size_t)a.B + q) * a.K_int,
+                           a.drop_rank0 && a.max_keys ? a.max_keys[q] : 0ull);
 }
 
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
@@ -668,10 +501,89 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
   if (a.counts && tid == 0) a.counts[q] = c;
 }
 
+// ---------------------------------------------------------------------------------------
+// Streaming bound from a kScanPilot scan (scan4_kernel.h): each query row's K-th largest
+// eligible half-tile maximum over the pilot rows.  The values come from K distinct half
+// tiles, so K distinct eligible items score at least that much: it bounds the K-th score
+// of the pilot sample — and of the whole index — from below, as the exact pilot list's
+// K-th key did (the stream then appends every eligible score reaching it).  One workgroup
+// per row: up to 16 values per thread, bitwise search of the K-th largest with ballot
+// counts and one LDS exchange per bit.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pilot_bound_kernel(const uint32_t* top, int n_chunks, int m, int nb, int K,
+                                                          uint64_t* thr_out) {
+  constexpr int kPer = 16;  // values per thread: 2·n_chunks·m <= 4096
+  __shared__ uint32_t xch[16];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int blk = row >> 5, r = row & 31;
+  const int nv = 2 * n_chunks * m;  // (chunk, half, i) -> ((chunk·nb + blk)·64 + half·32 + r)·m + i
+  uint32_t v[kPer];
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int j = tid + e * 256;
+    uint32_t x = 0;
+    if (j < nv) {
+      const int i = j % m, ch = j / m, c = ch >> 1, hh = ch & 1;
+      x = top[((size_t)(c * nb + blk) * 64 + hh * 32 + r) * m + i];
+    }
+    v[e] = x;
+  }
+  auto wave_count_ge = [&](uint32_t c) -> uint32_t {
+    uint32_t n = 0;
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) n += (uint32_t)__popcll(__ballot(v[e] >= c));
+    return n;
+  };
+  uint32_t hi = 0, lo = 0xFFFFFFFFu;
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    hi = max(hi, v[e]);
+    lo = v[e] ? min(lo, v[e]) : lo;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+    lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+  }
+  const uint32_t c1 = wave_count_ge(1u);
+  if (lane == 0) {
+    xch[8 + wave] = hi;
+    xch[12 + wave] = lo;
+    xch[wave] = c1;
+  }
+  __syncthreads();
+  const uint32_t H = max(max(xch[8], xch[9]), max(xch[10], xch[11]));
+  const uint32_t Lo = min(min(xch[12], xch[13]), min(xch[14], xch[15]));
+  uint32_t P = 0;  // 0 = fewer than K values: take every eligible item
+  if (xch[0] + xch[1] + xch[2] + xch[3] >= (uint32_t)K) {
+    const uint32_t d = H ^ Lo;
+    const int top_bit = d ? 31 - __builtin_clz(d) : -1;
+    P = top_bit < 0 ? H : H & ~((2u << top_bit) - 1u);
+    for (int bit = top_bit, st = 1; bit >= 0; --bit, ++st) {
+      const uint32_t c = P | (1u << bit);
+      const uint32_t wc = wave_count_ge(c);
+      uint32_t* slot = xch + 4 * (st & 1);
+      if (lane == 0) slot[wave] = wc;
+      __syncthreads();
+      if (slot[0] + slot[1] + slot[2] + slot[3] >= (uint32_t)K) P = c;
+    }
+  }
+  if (tid == 0) thr_out[row] = (uint64_t)P << 32;
+}
+
+hipError_t launch_pilot_bound(const uint32_t* top, int n_chunks, int m, int nb, int K, int B, uint64_t* thr_out,
+                              hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (!top || !thr_out || n_chunks <= 0 || m <= 0 || 2 * n_chunks * m > 16 * 256 || K <= 0 || B > 32 * nb)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pilot_bound_kernel, dim3(B), dim3(256), 0, s, top, n_chunks, m, nb, K, thr_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
   if (a.n_rows > a.B || a.P * a.K_int > kFinMerge || a.K_int > kMaxKInt || a.sides < 1 || a.sides > 2) return hipErrorInvalidValue;
-  static const bool legacy = getenv("BB_FINALIZE_LEGACY") != nullptr;
+  static const bool legacy = ab_env("BB_FINALIZE_LEGACY") != nullptr;
   if (a.P == 1 && !legacy)
     hipLaunchKernelGGL(finalize1_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
   else

@@ -7,7 +7,7 @@
 namespace bb {
 
 static bool scan4_env_off() {
-  static const bool off = getenv("BB_NO_SCAN4") != nullptr;
+  static const bool off = ab_env("BB_NO_SCAN4") != nullptr;
   return off;
 }
 
@@ -16,7 +16,7 @@ static bool scan4_env_off() {
 // (measured at 25,216 x 384, B=256: 20.5 vs 23.6 us per launch, 13.3M vs 7.4M q/s with
 // three batches in flight, profiles/r02c_b2.jsonl).
 bool scan4_used(int dtype, int Mpad) {
-  static const int min_rows = getenv("BB_SCAN4_MIN") ? atoi(getenv("BB_SCAN4_MIN")) : 512;
+  static const int min_rows = ab_env("BB_SCAN4_MIN") ? atoi(ab_env("BB_SCAN4_MIN")) : 512;
   return dtype == BF16 && Mpad % kScan4Queries == 0 && Mpad >= min_rows && !scan4_env_off();
 }
 
@@ -41,6 +41,8 @@ static void launch_t(const GemmArgs& a, hipStream_t s) {
   }
   if (a.cand)
     hipLaunchKernelGGL((scan4_kernel<KU, kScanStream>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+  else if (a.pilot_top)  // streaming pilot: top-m half-tile maxima, no image
+    hipLaunchKernelGGL((scan4_kernel<KU, kScanPilot>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
   else
     hipLaunchKernelGGL((scan4_kernel<KU>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
 }
@@ -86,6 +88,10 @@ hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t
   }
   return ok ? hipGetLastError() : hipErrorInvalidValue;
 }
+
+// top-m per lane of a kScanPilot scan4 launch of this row width (the interleaved schedule has
+// registers for 8, the chained d = 768 one for 4)
+int scan4_pilot_m(int kpad) { return kpad * 2 / 16 <= 64 ? 8 : 4; }
 
 bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s) {
   switch (ku) {

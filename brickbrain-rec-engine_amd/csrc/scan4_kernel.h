@@ -128,7 +128,8 @@ constexpr int scan4_atA(int s, int U, int E, int pieces) {
 
 // ABL (tools/scan4_probe only): 1 = no epilogue, 2 = no staging after the first tile, 4 = no
 // per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no streaming
-// appends (compares only), 64 = streaming appends without their stores.
+// appends (compares only), 64 = streaming appends without their stores, 2048 = no query
+// loads (zero operand).
 template <int KU, int ABL = 0, bool PM = false>
 __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int tiles_total, int L) {
   typedef uint16_t T;
@@ -215,15 +216,34 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
         rowp[b] = (const char*)a.Q + (size_t)(ok[b] ? q : 0) * a.ldq * sizeof(T);
       }
     }
+    // lane-order operand (q_perm, prep wrote every row up to Mpad): 1 KiB per wave load.
+    // Loads go out in batches of kQB plain loads before the batch's AGPR pinning: with the
+    // pinning asm between consecutive loads the compiler waited for each load on its own
+    // (one L2 round trip per query register).  (Inline-asm loads with a separate wait are
+    // NOT safe here: the compiler may copy or reuse a destination register before the wait.)
+    const uint4* qp = (const uint4*)a.Q + ((size_t)(group * 4 + wave) * (2 * U)) * 64 + lane;
+    constexpr int kQB = 16;
 #pragma unroll
-    for (int j = 0; j < 2 * U; ++j) {
-      const int b = j / U, u = j % U;
-      const uint4 v = *(const uint4*)(rowp[b] + (2 * u + h) * 16);
-      qv[j] = ok[b] ? __builtin_bit_cast(u32x4v, v) : u32x4v{0, 0, 0, 0};
-      if (j < NA)
-        asm volatile("" : "+a"(qv[j]));
-      else
-        asm volatile("" : "+v"(qv[j]));
+    for (int j0 = 0; j0 < 2 * U; j0 += kQB) {
+      uint4 t[kQB];
+#pragma unroll
+      for (int jj = 0; jj < kQB; ++jj) {
+        const int j = j0 + jj, b = j / U, u = j % U;
+        if (j >= 2 * U) continue;
+        t[jj] = (ABL & 2048) ? make_uint4(0u, 0u, 0u, 0u)
+                : a.q_perm   ? qp[(size_t)j * 64]
+                             : *(const uint4*)(rowp[b] + (2 * u + h) * 16);
+      }
+#pragma unroll
+      for (int jj = 0; jj < kQB; ++jj) {
+        const int j = j0 + jj, b = j / U;
+        if (j >= 2 * U) continue;
+        qv[j] = ok[b] || a.q_perm ? __builtin_bit_cast(u32x4v, t[jj]) : u32x4v{0, 0, 0, 0};
+        if (j < NA)
+          asm volatile("" : "+a"(qv[j]));
+        else
+          asm volatile("" : "+v"(qv[j]));
+      }
     }
   }
 
@@ -261,6 +281,30 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   auto list_put = [&](int period, const uint4& vA, const uint4& vB) __attribute__((always_inline)) {
     if (liveA) *(uint4*)(a.lists + 4 * list_slot(chunk, period, a.l_np, l_nb, qA >> 5, lane)) = vA;
     if (liveB) *(uint4*)(a.lists + 4 * list_slot(chunk, period, a.l_np, l_nb, qB >> 5, lane)) = vB;
+  };
+  // streaming pilot (kScanPilot): per block the lane's top-PM eligible half-tile maxima
+  constexpr bool PILOT = (ABL & kScanPilot) != 0 && !STREAM && !S16 && !LIST;
+  constexpr int kPM = IL ? 8 : 4;  // (the chained d = 768 schedule has no registers for more)
+  uint32_t pmA[kPM], pmB[kPM];
+#pragma unroll
+  for (int i = 0; i < kPM; ++i) pmA[i] = pmB[i] = 0u;
+  auto pm_ins = [&](uint32_t (&t)[kPM], uint32_t v) __attribute__((always_inline)) {
+    uint32_t n[kPM];
+    n[0] = maxu(t[0], v);
+#pragma unroll
+    for (int i = 1; i < kPM; ++i) n[i] = med3u(t[i - 1], t[i], v);
+#pragma unroll
+    for (int i = 0; i < kPM; ++i) t[i] = n[i];
+  };
+  auto pm_store = [&]() __attribute__((always_inline)) {
+    const int nbq = a.Mpad >> 5;
+    uint32_t* oA = a.pilot_top + ((size_t)(chunk * nbq + (qA >> 5)) * 64 + lane) * kPM;
+    uint32_t* oB = a.pilot_top + ((size_t)(chunk * nbq + (qB >> 5)) * 64 + lane) * kPM;
+#pragma unroll
+    for (int i = 0; i < kPM; i += 4) {
+      *(uint4*)(oA + i) = make_uint4(pmA[i], pmA[i + 1], pmA[i + 2], pmA[i + 3]);
+      *(uint4*)(oB + i) = make_uint4(pmB[i], pmB[i + 1], pmB[i + 2], pmB[i + 3]);
+    }
   };
   Stream4 slA, slB;
   auto region = [&](int q) __attribute__((always_inline)) { return ((size_t)q * n_chunks + chunk) * 2 + h; };
@@ -316,6 +360,12 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
         any = __any(te >= sl.thr);
         ep = s4_elig16(ok, ptile0, a.n_valid, h);
       }
+      if constexpr (PILOT) {
+        if (q == qA) pm_ins(pmA, te);
+        else pm_ins(pmB, te);
+      }
+    } else if constexpr (PILOT) {
+      // (no score image, no maxima rows: the lane's top-PM list is the pilot's output)
     } else if constexpr (STREAM) {
       if constexpr (s <= 4) {
         if (any) {
@@ -394,7 +444,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   constexpr int kSlicesA = PIECES + 1 + kEpi;
   // End of a tile: wait for the LDS-DMA of the next tile, not for block A's score-image
   // stores issued after it (vmcnt counts loads, stores and LDS-DMA together, in order).
-  constexpr bool kStores = !STREAM && !LIST && !(ABL & (1 | 8));
+  constexpr bool kStores = !STREAM && !LIST && !PILOT && !(ABL & (1 | 8));
 
   // One tile: chain A over buffer BUF (+ block B's epilogue of tile-1 when EPIB), chain B
   // (+ block A's epilogue of this tile).
@@ -659,6 +709,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       last(accA, accB);
     else
       last(accA1, accB1);
+    if constexpr (PILOT) pm_store();
     if constexpr (STREAM) {
       a.cand_cnt[region(qA)] = slA.n;
       a.cand_cnt[region(qB)] = slB.n;
@@ -685,6 +736,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     bool any = false;
     static_for<kEpi>([&](auto SL) { epi_slice(SL, accB, tile - 1, ppw, pmw, pewB, qB, slB, te, tp, ep, any); });
   }
+  if constexpr (PILOT) pm_store();
   if constexpr (STREAM) {
     a.cand_cnt[region(qA)] = slA.n;
     a.cand_cnt[region(qB)] = slB.n;

@@ -1138,7 +1138,7 @@ hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s) {
       (a.max_inout && !a.pmax) || (a.slab_start & 31) || (a.out_scores && a.k_final > kWvCand))
     return hipErrorInvalidValue;
   // two waves per SIMD at most for the fat variant: 256 CUs x 4 SIMDs x 2
-  static const int um_env = getenv("BB_WAVE_UM") ? atoi(getenv("BB_WAVE_UM")) : 0;
+  static const int um_env = ab_env("BB_WAVE_UM") ? atoi(ab_env("BB_WAVE_UM")) : 0;
   const bool fat = um_env ? um_env == 2 : true;
   if (fat)
     hipLaunchKernelGGL(select_rr_wave_kernel<2>, dim3(B), dim3(64), 0, s, a);
@@ -1189,7 +1189,7 @@ hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s) {
     hipLaunchKernelGGL((select_kernel<0, true>), dim3(B), dim3(kSelectThreads), 0, s, a);
     return hipGetLastError();
   }
-  static const int abl = getenv("BB_SELECT_ABLATE") ? atoi(getenv("BB_SELECT_ABLATE")) : 0;
+  static const int abl = ab_env("BB_SELECT_ABLATE") ? atoi(ab_env("BB_SELECT_ABLATE")) : 0;
   switch (abl) {
     case 1: hipLaunchKernelGGL(select_kernel<1>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
     case 2: hipLaunchKernelGGL(select_kernel<2>, dim3(B), dim3(kSelectThreads), 0, s, a); break;

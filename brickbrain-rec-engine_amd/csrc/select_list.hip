@@ -35,7 +35,7 @@ constexpr int kLsCand = 2048;   // rescore buffer (u64 keys): candidates + overf
 constexpr int kLsFlush = 1024;  // fallback: batch size that triggers a merge of the running top-K
 constexpr int kLsSeg = 64;      // overflowed lists
 constexpr int kLsR0Seg = 64;    // rank-0 segments
-constexpr int kLsMaxLists = 1024;
+constexpr int kLsMaxLists = kListMaxPerRow;
 constexpr int kLsOffCand = 0;
 constexpr int kLsOffSel = kLsOffCand + kLsCand * 8;          // u64 [kMaxKInt] running top-K (fallback)
 constexpr int kLsOffHist = kLsOffSel + kMaxKInt * 8;         // u32 [256] bound histogram
@@ -101,16 +101,18 @@ __device__ __forceinline__ void ls_append(const uint32_t* seg, int ns, uint64_t*
   }
 }
 
-// The rescore of the list select: one pass, as many rows in flight as the registers allow
-// (one select wave per SIMD; the scan of the next batch cannot share the CU anyway).
+// The rescore of the list select: 32 rows in flight per workgroup at d = 384, the query
+// chunks re-read from LDS each round — the kernel fits 170 VGPRs, three workgroups per CU
+// (the hybrid select runs 2·B of them; the gathers are bound by the chip's bandwidth, not by
+// rows in flight).
 __device__ __forceinline__ void ls_rescore(uint64_t* keys, int m, const SelectArgs& a, const float* qs) {
   const int cpl = ((a.rr_d >> 2) + 15) >> 4;
   const int t = threadIdx.x;
-  if (cpl <= 1) rescore_rows<1, 16, 16>(keys, m, a, qs, t);
-  else if (cpl <= 2) rescore_rows<2, 8, 16>(keys, m, a, qs, t);
-  else if (cpl <= 4) rescore_rows<4, 4, 16>(keys, m, a, qs, t);
-  else if (cpl <= 6) rescore_rows<6, 4, 16>(keys, m, a, qs, t);
-  else rescore_rows<8, 2, 16>(keys, m, a, qs, t);   // rows up to kRrMaxD = 512 wide
+  if (cpl <= 1) rescore_rows<1, 8, 16, false>(keys, m, a, qs, t);
+  else if (cpl <= 2) rescore_rows<2, 4, 16, false>(keys, m, a, qs, t);
+  else if (cpl <= 4) rescore_rows<4, 2, 16, false>(keys, m, a, qs, t);
+  else if (cpl <= 6) rescore_rows<6, 2, 16, false>(keys, m, a, qs, t);
+  else rescore_rows<8, 1, 16, false>(keys, m, a, qs, t);   // rows up to kRrMaxD = 512 wide
 }
 
 __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
@@ -363,79 +365,79 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
       a.trace[row * 16 + 9] = (uint64_t)(Mc - (int)ncand0) | ((uint64_t)(M - Mc) << 32);
     }
     // ranks by counting: key i's position = #keys larger (keys are distinct: distinct ids);
-    // every thread ranks its keys against the whole buffer with broadcast LDS reads, 16 keys
-    // per step with the next 16 already in flight (LDS latency bounds this loop).  The
+    // every thread ranks its keys against the whole buffer with broadcast LDS reads, 8 keys
+    // per step with the next 8 already in flight (LDS latency bounds this loop).  The
     // buffer is zero-padded to a multiple of 16 first (the rank-0 items there are consumed).
     const int Mc16 = (Mc + 15) & ~15;
     __syncthreads();
     if (tid < Mc16 - Mc) cand[Mc + tid] = 0ull;
-    constexpr int kRk = kLsCand / kSelectThreads;
-    uint64_t mk[kRk];
-    uint32_t rk[kRk];
-#pragma unroll
-    for (int e = 0; e < kRk; ++e) {
-      const int i = tid + e * kSelectThreads;
-      mk[e] = i < Mc ? cand[i] : 0ull;
-      rk[e] = 0;
-    }
-    __syncthreads();
-    const int ne = (Mc + kSelectThreads - 1) / kSelectThreads;  // uniform
+    const int ne = (Mc + kSelectThreads - 1) / kSelectThreads;  // keys per thread (uniform)
     const ulonglong2* c2 = (const ulonglong2*)cand;
-    auto rank_pass = [&](auto NE) __attribute__((always_inline)) {
+    const int cnt = min(Mc, K);
+    // one instance per keys-per-thread count E: only its own E keys and ranks live
+    auto rank_emit = [&](auto NE) __attribute__((always_inline)) {
       constexpr int E = decltype(NE)::value;
-      ulonglong2 ya[8], yb[8];
+      uint64_t mk[E];
+      uint32_t rk[E];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) ya[jj] = c2[jj];
-      for (int k = 0; k < Mc16; k += 16) {
-        const int kn = k + 16 < Mc16 ? k + 16 : k;  // (the last step re-reads, harmlessly)
+      for (int e = 0; e < E; ++e) {
+        const int i = tid + e * kSelectThreads;
+        mk[e] = i < Mc ? cand[i] : 0ull;
+        rk[e] = 0;
+      }
+      __syncthreads();
+      ulonglong2 ya[4], yb[4];
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) yb[jj] = c2[(kn >> 1) + jj];
+      for (int jj = 0; jj < 4; ++jj) ya[jj] = c2[jj];
+      for (int k = 0; k < Mc16; k += 8) {
+        const int kn = k + 8 < Mc16 ? k + 8 : k;  // (the last step re-reads, harmlessly)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) yb[jj] = c2[(kn >> 1) + jj];
 #pragma unroll
         for (int e = 0; e < E; ++e)
 #pragma unroll
-          for (int jj = 0; jj < 8; ++jj) rk[e] += (ya[jj].x > mk[e] ? 1u : 0u) + (ya[jj].y > mk[e] ? 1u : 0u);
+          for (int jj = 0; jj < 4; ++jj) rk[e] += (ya[jj].x > mk[e] ? 1u : 0u) + (ya[jj].y > mk[e] ? 1u : 0u);
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) ya[jj] = yb[jj];
+        for (int jj = 0; jj < 4; ++jj) ya[jj] = yb[jj];
+      }
+      if (a.out_scores) {
+        // rank 0 dropped when it heads the list (the head is the unmasked arg-max iff that
+        // item is eligible: gmax is then among the candidates)
+        if (tid == 0) misc[M_BUF] = 0u;
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (tid + e * kSelectThreads < Mc && rk[e] == 0 && gmax && mk[e] == gmax) misc[M_BUF] = 1u;
+        __syncthreads();
+        const int start = (int)misc[M_BUF];
+        const int c = min(a.k_final, cnt - start);
+        float* sc = a.out_scores + (size_t)row * a.k_final;
+        int64_t* id = a.out_ids + (size_t)row * a.k_final;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int pos = (int)rk[e] - start;
+          if (tid + e * kSelectThreads < Mc && pos >= 0 && pos < c) {
+            sc[pos] = float_of_ord(ordk_of(mk[e]));
+            id[pos] = (int64_t)gid_of(mk[e]);
+          }
+        }
+        for (int i = c + tid; i < a.k_final; i += kSelectThreads) {
+          sc[i] = 0.f;
+          id[i] = -1;
+        }
+        if (a.out_counts && tid == 0) a.out_counts[row] = c;
+      } else {
+        uint64_t* out = a.keys_out + (size_t)row * K;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (tid + e * kSelectThreads < Mc && rk[e] < (uint32_t)K) out[rk[e]] = mk[e];
+        for (int i = cnt + tid; i < K; i += kSelectThreads) out[i] = 0ull;
       }
     };
-    if (ne <= 1) rank_pass(std::integral_constant<int, 1>{});
-    else if (ne <= 2) rank_pass(std::integral_constant<int, 2>{});
-    else if (ne <= 4) rank_pass(std::integral_constant<int, 4>{});
-    else rank_pass(std::integral_constant<int, kRk>{});
-    const int cnt = min(Mc, K);
-    if (a.out_scores) {
-      // rank 0 dropped when it heads the list (the head is the unmasked arg-max iff that item
-      // is eligible: gmax is then among the candidates)
-      if (tid == 0) misc[M_BUF] = 0u;
-      __syncthreads();
-#pragma unroll
-      for (int e = 0; e < kRk; ++e)
-        if (e < ne && tid + e * kSelectThreads < Mc && rk[e] == 0 && gmax && mk[e] == gmax) misc[M_BUF] = 1u;
-      __syncthreads();
-      const int start = (int)misc[M_BUF];
-      const int c = min(a.k_final, cnt - start);
-      float* sc = a.out_scores + (size_t)row * a.k_final;
-      int64_t* id = a.out_ids + (size_t)row * a.k_final;
-#pragma unroll
-      for (int e = 0; e < kRk; ++e) {
-        const int pos = (int)rk[e] - start;
-        if (e < ne && tid + e * kSelectThreads < Mc && pos >= 0 && pos < c) {
-          sc[pos] = float_of_ord(ordk_of(mk[e]));
-          id[pos] = (int64_t)gid_of(mk[e]);
-        }
-      }
-      for (int i = c + tid; i < a.k_final; i += kSelectThreads) {
-        sc[i] = 0.f;
-        id[i] = -1;
-      }
-      if (a.out_counts && tid == 0) a.out_counts[row] = c;
-    } else {
-      uint64_t* out = a.keys_out + (size_t)row * K;
-#pragma unroll
-      for (int e = 0; e < kRk; ++e)
-        if (e < ne && tid + e * kSelectThreads < Mc && rk[e] < (uint32_t)K) out[rk[e]] = mk[e];
-      for (int i = cnt + tid; i < K; i += kSelectThreads) out[i] = 0ull;
-    }
+    if (ne <= 1) rank_emit(std::integral_constant<int, 1>{});
+    else if (ne <= 2) rank_emit(std::integral_constant<int, 2>{});
+    else if (ne <= 4) rank_emit(std::integral_constant<int, 4>{});
+    else rank_emit(std::integral_constant<int, kLsCand / kSelectThreads>{});
     stamp(7);
     return;
   }
@@ -449,7 +451,7 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     __syncthreads();
     uint64_t best = 0;
     auto r0_reduce = [&](int nb) {
-      rr_rescore_any(rb, nb, a, qs);
+      ls_rescore(rb, nb, a, qs);
       __syncthreads();
       for (int i = tid; i < nb; i += kSelectThreads) best = rb[i] > best ? rb[i] : best;
       __syncthreads();
@@ -472,7 +474,7 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   if (tid == 0) misc[M_BUF] = 0u;
   __syncthreads();
   auto merge = [&](int nb) {
-    rr_rescore_any(cand, nb, a, qs);
+    ls_rescore(cand, nb, a, qs);
     __syncthreads();
     for (int i = tid; i < K; i += kSelectThreads) cand[nb + i] = sel[i];
     int P = 1;
@@ -506,11 +508,11 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   for (int i = tid; i < K; i += kSelectThreads) out[i] = sel[i];
 }
 
-__global__ __launch_bounds__(kSelectThreads) void select_list_kernel(SelectArgs a, int B) {
+__global__ __launch_bounds__(kSelectThreads) __attribute__((amdgpu_waves_per_eu(3))) void select_list_kernel(SelectArgs a, int B) {
   select_list_body(a, xcd_row(blockIdx.x, B));
 }
 // both sides of a hybrid search: workgroups [0, B) side 0, the rest side 1
-__global__ __launch_bounds__(kSelectThreads) void select_list_dual_kernel(SelectArgs a0, SelectArgs a1, int B) {
+__global__ __launch_bounds__(kSelectThreads) __attribute__((amdgpu_waves_per_eu(3))) void select_list_dual_kernel(SelectArgs a0, SelectArgs a1, int B) {
   if ((int)blockIdx.x < B)
     select_list_body(a0, xcd_row(blockIdx.x, B));
   else

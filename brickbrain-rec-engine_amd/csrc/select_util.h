@@ -2,6 +2,8 @@
 // score-slab loads, block scans, radix select, register bitonic sorts and the exact f32
 // rescoring of candidate rows (f64 sums in one fixed order).
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace bb {
@@ -313,23 +315,29 @@ __device__ __forceinline__ uint64_t rr_key(float e, uint32_t gid) { return make_
 // 16 (NG·16 threads call it together), U rows per group in flight (U·CPL <= 12 chunks per
 // lane: the select's register budget, not its row latency, bounds the in-flight throughput —
 // a fat select wave keeps the next batch's scan off the CU).
-template <int CPL, int U, int NG>
+template <int CPL, int U, int NG, bool QF64 = true>
 __device__ __forceinline__ void rescore_rows(uint64_t* keys, int m, const SelectArgs& a, const float* qs, int t) {
   const int p = t & 15, g = t >> 4;
   const int nch = a.rr_d >> 2;
-  // the query chunks of this lane in f64 (zero past the row: those FMAs add exact zeros, so
-  // the sum — and its order — is the same for every row width; no per-chunk branches, which
-  // put every FMA in a basic block of its own behind its own s_waitcnt)
-  double qd[CPL][4];
+  // the query chunks of this lane (zero past the row: those FMAs add exact zeros, so the sum
+  // — and its order — is the same for every row width; no per-chunk branches, which put
+  // every FMA in a basic block of its own behind its own s_waitcnt); widened to f64 once
+  // (QF64) or at each use (half the registers: occupancy of the list select)
+  // (the lean variant re-reads its query chunks from LDS every round: the compiler hoists
+  // any register copy's f32 -> f64 conversions out of the loop, 2·4·CPL registers)
+  double qd[QF64 ? CPL : 1][4];
+  auto load_q = [&]() __attribute__((always_inline)) {
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    const int c = p + 16 * j;
-    const f4v q = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
-    qd[j][0] = (double)q.x;
-    qd[j][1] = (double)q.y;
-    qd[j][2] = (double)q.z;
-    qd[j][3] = (double)q.w;
-  }
+    for (int j = 0; j < (QF64 ? CPL : 1); ++j) {
+      const int c = p + 16 * j;
+      const f4v q = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
+      qd[j][0] = (double)q.x;
+      qd[j][1] = (double)q.y;
+      qd[j][2] = (double)q.z;
+      qd[j][3] = (double)q.w;
+    }
+  };
+  if constexpr (QF64) load_q();
   for (int c0 = g * U; c0 < m; c0 += NG * U) {
     uint32_t gid[U];
     f4v xv[U][CPL];
@@ -342,15 +350,27 @@ __device__ __forceinline__ void rescore_rows(uint64_t* keys, int m, const Select
 #pragma unroll
       for (int j = 0; j < CPL; ++j) xv[u][j] = xr[min(p + 16 * j, nch - 1)];
     }
+    f4v ql[QF64 ? 1 : CPL];
+    if constexpr (!QF64) {
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const int c = p + 16 * j;
+        ql[j] = c < nch ? lds_f4(qs, c) : f4v{0.f, 0.f, 0.f, 0.f};
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       double acc = 0.0;
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
-        acc = fma((double)xv[u][j].x, qd[j][0], acc);
-        acc = fma((double)xv[u][j].y, qd[j][1], acc);
-        acc = fma((double)xv[u][j].z, qd[j][2], acc);
-        acc = fma((double)xv[u][j].w, qd[j][3], acc);
+        const double q0 = QF64 ? qd[QF64 ? j : 0][0] : (double)ql[QF64 ? 0 : j].x;
+        const double q1 = QF64 ? qd[QF64 ? j : 0][1] : (double)ql[QF64 ? 0 : j].y;
+        const double q2 = QF64 ? qd[QF64 ? j : 0][2] : (double)ql[QF64 ? 0 : j].z;
+        const double q3 = QF64 ? qd[QF64 ? j : 0][3] : (double)ql[QF64 ? 0 : j].w;
+        acc = fma((double)xv[u][j].x, q0, acc);
+        acc = fma((double)xv[u][j].y, q1, acc);
+        acc = fma((double)xv[u][j].z, q2, acc);
+        acc = fma((double)xv[u][j].w, q3, acc);
       }
       acc = sum16_f64(acc);
       if (p == 0 && c0 + u < m) keys[c0 + u] = rr_key((float)acc, gid[u]);

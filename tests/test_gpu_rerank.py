@@ -209,7 +209,7 @@ np.savez(sys.argv[3], sc=sc, ids=ids, s2=s2, i2=i2)
     for fused in ("0", "1"):
         path = os.path.join(root, "gpurun_out", f"rr_fused_{fused}.npz")
         os.makedirs(os.path.dirname(path), exist_ok=True)
-        env = dict(os.environ, BB_RR_FUSED=fused)
+        env = dict(os.environ, BB_AB="1", BB_RR_FUSED=fused)   # A/B switches need BB_AB
         subprocess.run([sys.executable, "-c", code, root, pkg, path], check=True, env=env, timeout=120)
         out[fused] = np.load(path)
     for key in ("sc", "ids", "s2", "i2"):

@@ -40,7 +40,7 @@ for M in ${MODES//+/ }; do
       i=0
       for e in "${ENVS[@]}"; do
         i=$((i+1))
-        timeout -k 10 300 env $e python3 bench.py --no-cpu "${ARGS[@]}" > "$O/bench_$i.log" 2>&1; rc=$?
+        timeout -k 10 300 env BB_AB=1 $e python3 bench.py --no-cpu "${ARGS[@]}" > "$O/bench_$i.log" 2>&1; rc=$?
         [ $rc -ne 0 ] && { echo "bench[$e] rc=$rc"; tail -5 "$O/bench_$i.log"; exit $rc; }
         summ "$O/bench_$i.log" "$e"
       done ;;
