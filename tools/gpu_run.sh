@@ -6,6 +6,7 @@
 #   bash tools/gpu_run.sh TAG ablib [ARGS]              this tree's library vs tools/ab/libbrickrec_head.so, alternating
 #   bash tools/gpu_run.sh TAG prof [ARGS]               rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   bash tools/gpu_run.sh TAG pmc [ARGS]                PMC passes (one counter group per run) of bench.py ARGS
+#   bash tools/gpu_run.sh TAG traffic [ARGS]            the FETCH_SIZE and WRITE_SIZE passes only
 #
 # Several modes chain with "+": bash tools/gpu_run.sh r03a tests+bench+prof --workload c3
 # Every GPU step runs under its own timeout; the first abnormal exit ends the script.
@@ -58,11 +59,13 @@ for M in ${MODES//+/ }; do
           --output-format csv -- python3 "$R/bench.py" --no-cpu --no-sweep "${ARGS[@]}" > "$O/prof.log" 2>&1 ); rc=$?
       echo "prof rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$O/prof.log"; exit $rc; }
       for f in $(find "$O/prof" -name "*kernel_stats.csv"); do head -12 "$f"; done ;;
-    pmc)
+    pmc|traffic)
       i=0
-      for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM" \
-                 "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVES" \
-                 "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+      PGROUPS=("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM"
+              "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVES"
+              "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT")
+      [ $M = traffic ] && PGROUPS=("FETCH_SIZE" "WRITE_SIZE")   # HBM bytes only
+      for grp in "${PGROUPS[@]}"; do
         i=$((i+1))
         ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$O/pmc/p$i" -o run \
             --output-format csv -- python3 "$R/bench.py" --steps 30 --warmup 5 --no-cpu --no-sweep --inflight 1 "${ARGS[@]}" \

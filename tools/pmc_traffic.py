@@ -16,7 +16,7 @@ import os
 import sys
 
 SCAN = ("bb::scan3_kernel", "bb::scan2_kernel", "bb::scan4_kernel", "bb::scan4_dual_kernel")
-ANCHOR = {"f32": ("bb::select_kernel", "bb::scan3_kernel"), "c3": ("bb::finalize1_kernel",),
+ANCHOR = {"f32": ("bb::select_list_kernel", "bb::select_kernel", "bb::scan3_kernel"), "c3": ("bb::finalize1_kernel",),
           "c4": ("bb::finalize_kernel", "bb::finalize1_kernel"), "c5": ("bb::finalize_kernel", "bb::finalize1_kernel")}
 
 
