@@ -473,6 +473,18 @@ def main():
              for j in range(args.inflight)]
     idx, stream, run, (o_sc, o_ids, o_cnt), q = lanes[0]
 
+    # ---- single-batch latency without other batches in flight (lane 0 alone, 200 batches) ----
+    # Measured before the warmup steps, so the timed window opens on a GPU that has been serving
+    # (a 20-step window otherwise starts on the clocks of the idle before it).
+    ser = []
+    for _ in range(200):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        run()
+        b.record(stream)
+        ser.append((a, b))
+    torch.cuda.synchronize()
+    lat_serial = np.array([a.elapsed_time(b) for a, b in ser])
     for i in range(args.warmup):
         lanes[i % len(lanes)][2]()
     torch.cuda.synchronize()
@@ -497,17 +509,6 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
-
-    # ---- single-batch latency without other batches in flight (lane 0 alone) ----
-    ser = []
-    for _ in range(min(args.steps, 200)):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        run()
-        b.record(stream)
-        ser.append((a, b))
-    torch.cuda.synchronize()
-    lat_serial = np.array([a.elapsed_time(b) for a, b in ser])
 
     # ---- per-kernel device time (HIP events on the launch stream), same K steps ----
     idx.set_profiling(True)

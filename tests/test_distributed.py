@@ -91,7 +91,7 @@ def _reference():
     return ref
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_sharded_matches_unsharded(world):
     from oracle import restatement as R
     ctx = mp.get_context("spawn")
