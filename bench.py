@@ -385,11 +385,11 @@ def make_lane(brickrec, workload, base, B, local, dev, rank, j, inflight, extra)
 
 
 def gpu_batch_sweep(brickrec, base, local, dev, seconds=0.5):
-    """GPU q/s (3 in flight) and serial p50 at B ∈ {1 (top-10), 256, 1024, 4096}: the
-    north_star's batch axis at 25K items."""
+    """GPU q/s (3 in flight) and serial p50 at B ∈ {1 (top-10), 16, 64, 256, 1024, 4096}:
+    the north_star's batch axis at 25K items."""
     import torch
     res = []
-    for b, kk in ((1, 10), (256, 50), (1024, 50), (4096, 50)):
+    for b, kk in ((1, 10), (16, 50), (64, 50), (256, 50), (1024, 50), (4096, 50)):
         lanes = []
         for j in range(3):
             idx = base.view()

@@ -689,7 +689,11 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     const int tpc = (tiles + nch - 1) / nch;
     if (nch > 256) return false;
     np = (tpc + kListMaxPeriod - 1) / kListMaxPeriod;
-    while (2 * nch * np < 3 * K_int && 2 * nch * (np + 1) <= kListMaxPerRow && np < tpc) ++np;
+    // BB_LIST_DENSE (A/B runs): as many periods as the per-row cap allows (shorter periods:
+    // fewer overflowed lists, and fewer items to enumerate when one overflows)
+    static const bool dense = ab_env("BB_LIST_DENSE") && atoi(ab_env("BB_LIST_DENSE")) != 0;
+    const int np_goal = dense ? kListMaxPerRow : 3 * K_int;
+    while (2 * nch * np < np_goal && 2 * nch * (np + 1) <= kListMaxPerRow && np < tpc) ++np;
     G = (tpc + np - 1) / np;
     np = (tpc + G - 1) / G;
     return G <= kListMaxPeriod && 2 * nch * np <= kListMaxPerRow;
@@ -856,6 +860,18 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     const bool lgeo = list_geom(bpad, l_nch, l_np, l_G);
     const bool list_c = lgeo && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
     const bool list_f = lgeo && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
+    // raw-query lists (semantic searches on scan2, f32 query rows, small chunks): the scan
+    // rounds the RAW rows to its bf16 operand and the list select normalises them and derives
+    // ε itself — no prep launch on the path.  Every item chunk's workgroups convert their
+    // query rows again, so it pays only for small chunks: at 256 rows (configs[1]) the scan
+    // grew 16.6 -> 20.4 us and three batches in flight served 8.8 instead of 10.2 M q/s,
+    // while the serial search fell 48 -> 43 us (r03_raw); serial B = 1 / 16: 30.0 -> 28.8 /
+    // 34.5 -> 33.0 us, B = 64 unchanged (r03_raw3).  BB_RR_RAW (A/B runs): 0 / 1 forces it
+    // off / on; auto = chunks of at most kRrRawRows rows.
+    static const int rr_raw_env = ab_env("BB_RR_RAW") ? atoi(ab_env("BB_RR_RAW")) : -1;
+    const bool rr_raw_on = rr_raw_env >= 0 ? rr_raw_env != 0 : bc <= kRrRawRows;
+    const bool rraw_c = rr_raw_on && list_c && q->mode == BB_MODE_SEMANTIC && !scan4_used(BF16, bpad) &&
+                        q->q_dtype == F32 && x->d % 4 == 0 && x->d <= kRrMaxD && rows_c && ((uintptr_t)rows_c & 15) == 0;
     const bool s16_c = !list_c && s16_on && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
     const bool s16_f = !list_f && s16_on && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
     const size_t list_side_b = (size_t)l_nch * l_np * (bpad / 32) * 64 * 16;
@@ -864,7 +880,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
          (list_c && drop && (rc = x->r0lists.ensure((size_t)l_nch * (bpad / 32) * 64 * 8)))))
       return rc;
     // the prep launches of both sides (hybrid) go out as one launch
-    const bool prep_c = need_content && !fuse_c && !rrfuse_c, prep_f = need_cf && !fuse_f && !rrfuse_f;
+    const bool prep_c = need_content && !fuse_c && !rrfuse_c && !rraw_c, prep_f = need_cf && !fuse_f && !rrfuse_f;
     PrepArgs pa_c{}, pa_f{};
     if (prep_c) {
       PrepArgs& pa = pa_c;
@@ -917,14 +933,17 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       pa.src_ld = x->r;
       pa.normalize = 0;
     }
-    // the bf16 operand of a scan4 launch goes out in its lane order (scan4_q_offset):
-    // coalesced prologue loads (at 1,024 x 384 the row-major loads took ~8 of a 23 us scan)
-    const bool perm_c = prep_c && !s3_c && scan4_used(BF16, bpad) &&
+    // the bf16 operand of a scan launch goes out in its lane order (scan4_q_offset /
+    // scan2_q_offset): coalesced prologue loads (at 1,024 x 384 the row-major loads took ~8
+    // of a 23 us scan4).  BB_QPERM2=0 (A/B runs) keeps scan2's row-major operand.
+    static const bool qperm2_env = !(ab_env("BB_QPERM2") && atoi(ab_env("BB_QPERM2")) == 0);
+    const int perm_kind = scan4_used(BF16, bpad) ? 1 : qperm2_env ? 2 : 0;
+    const bool perm_c = perm_kind && prep_c && !s3_c &&
                         (rr_c ? gemm_uses_scan(BF16, bpad, x->Dpad_b) : x->dtype == BF16 && scan_c);
-    const bool perm_f = prep_f && !s3_f && scan4_used(BF16, bpad) &&
+    const bool perm_f = perm_kind && prep_f && !s3_f &&
                         (rr_f ? gemm_uses_scan(BF16, bpad, x->Rpad_b) : x->dtype == BF16 && scan_f);
-    pa_c.q_perm = perm_c ? 1 : 0;
-    pa_f.q_perm = perm_f ? 1 : 0;
+    pa_c.q_perm = perm_c ? perm_kind : 0;
+    pa_f.q_perm = perm_f ? perm_kind : 0;
     if (prep_c && prep_f) {
       if ((rc = timed(x, K_PREP, s, [&] { return launch_prep2(pa_c, pa_f, s); }))) return rc;
     } else if (prep_c || prep_f) {
@@ -964,7 +983,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         const int ncols_pad = (int)round_up(ncols, kTileRows);
         GemmArgs ga{};
         ga.Q = cf_side ? x->qcf.p : x->qn.p;
-        ga.q_perm = (cf_side ? perm_f : perm_c) ? 1 : 0;
+        ga.q_perm = (cf_side ? perm_f : perm_c) ? perm_kind : 0;
         ga.ldq = cf_side ? x->Rpad : x->Dpad;
         ga.X = (const char*)(cf_side ? x->cf.p : x->items.p) + (size_t)c0 * ga.ldq * es;
         ga.ldx = ga.ldq;
@@ -1044,6 +1063,15 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           ga.Kpad = (int)w;
           ga.s_h = (cf_side ? s16_f || list_f : s16_c || list_c) ? (const float*)(cf_side ? x->qcfh.p : x->qh.p)
                                                                    : nullptr;
+          if (!cf_side && rraw_c) {
+            ga.q_raw = 1;
+            ga.q_src = rows_c;
+            ga.q_src_ld = x->d;
+            ga.q_d = x->d;
+            ga.q_istats = (const float*)x->rr_stats.p;
+            ga.q_h_out = (float*)x->qh.p;
+            ga.q_eps_out = (float*)x->qeps.p;
+          }
           if (cf_side ? list_f : list_c) {
             ga.lists = (uint32_t*)((char*)x->lists.p + (side ? list_side_b : 0));
             ga.r0lists = side_drop ? (uint32_t*)x->r0lists.p : nullptr;
@@ -1172,6 +1200,13 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           sa.l_np = l_np;
           sa.l_period = l_G;
           sa.l_nb = bpad / 32;
+          if (!cf_side && rraw_c) {
+            sa.rr_q_raw = rows_c;
+            sa.rr_q_raw_ld = x->d;
+            sa.rr_q_raw_d = x->d;
+          }
+          static const int ls_ablate = ab_env("BB_LS_ABLATE") ? atoi(ab_env("BB_LS_ABLATE")) : 0;
+          sa.ablate = ls_ablate;
           final_pp = pp;
           if (q->mode == BB_MODE_HYBRID && side == 0 && list_f) {
             sa_dual0 = sa;  // launched with side 1's

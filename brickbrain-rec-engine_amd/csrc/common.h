@@ -84,6 +84,13 @@ struct GemmArgs {
   float* q_f32_out;         // [Mpad][q_f32_ld]
   int64_t q_f32_ld;
   float* q_eps_out;         // [Mpad]
+  // raw-query re-rank prologue (q_raw; scan2, bf16, list epilogue, semantic search): the bf16
+  // operand is the RAW f32 row q_src rounded (no normalisation — a positive scale per query
+  // never reorders its items), with the code quantum h derived from the row's norm
+  // (scan2_raw_prologue; q_istats = the item statistics); the workgroups of item chunk 0
+  // write h (q_h_out) and the raw-unit bound ε' (q_eps_out).  The list select normalises
+  // the row itself (qnorm.h, as prep_kernel): no prep launch.
+  int32_t q_raw;
   uint64_t* trace;          // probe builds only (scan3 ABL & 256): per-workgroup timestamps
   // streaming top-K (scan ABL & kScanStream): no S slab; every eligible score whose order
   // image reaches the query's bound is appended to a private per-lane candidate region
@@ -106,7 +113,7 @@ struct GemmArgs {
   uint32_t* lists;          // uint4 at list_slot(chunk, period, l_np, Mpad/32, q >> 5, lane)
   uint32_t* r0lists;        // uint2 at list_slot(chunk, 0, 1, Mpad/32, q >> 5, lane), or null
   int32_t l_period, l_np;
-  int32_t q_perm;           // scan4: Q holds the prepped operand in lane order (scan4_q_offset)
+  int32_t q_perm;           // Q holds the prepped operand in lane order: 1 = scan4's (scan4_q_offset), 2 = scan2's
   // streaming pilot (scan ABL kScanPilot): no score image; per lane the top pilot_m of its
   // eligible half-tile maxima over the item chunk, u32 order images at
   // ((chunk·(Mpad/32) + q/32)·64 + lane)·pilot_m (pilot_bound_kernel turns them into bounds)
@@ -120,6 +127,13 @@ struct GemmArgs {
 __host__ __device__ inline size_t scan4_q_offset(int q, int c, int U) {  // in 16-B units
   const int g = q >> 8, w = (q >> 6) & 3, b = (q >> 5) & 1, r = q & 31, u = c >> 1, h = c & 1;
   return ((size_t)(g * 4 + w) * (2 * U) + b * U + u) * 64 + h * 32 + r;
+}
+// The scan2 query operand in lane order (q_perm == 2): chunk c = 2u + h of query row q sits
+// where lane (r = q & 31, h) of the wave holding rows 32·(q >> 5) .. +32 loads it at u-step
+// u, so each prologue load of a wave reads 1 KiB contiguous (row-major: 64 pieces of 16 B
+// from 32 rows).
+__host__ __device__ inline size_t scan2_q_offset(int q, int c, int U) {  // in 16-B units
+  return ((size_t)(q >> 5) * U + (c >> 1)) * 64 + (c & 1) * 32 + (q & 31);
 }
 constexpr int kScanStream = 512;  // scan ABL bit: streaming top-K epilogue
 constexpr int kScanS16 = 4096;    // scan ABL bit: int16 score image (GemmArgs.s_h)
@@ -252,10 +266,18 @@ struct SelectArgs {
   const uint32_t* lists;
   const uint32_t* r0lists;
   int32_t l_chunks, l_tiles, l_np, l_period, l_nb;
+  int32_t ablate;           // probe runs (BB_LS_ABLATE): 1 = every rescore gathers row 0 (cache-resident)
+  // raw-query lists (GemmArgs.q_raw): the select normalises row rr_q_raw[row] (real width
+  // rr_q_raw_d, stride rr_q_raw_ld) into its LDS query with prep_kernel's arithmetic
+  // (qnorm.h); rr_eps = the scan's raw-unit bound, s_h its quantum; rr_q is not read
+  const float* rr_q_raw;
+  int64_t rr_q_raw_ld;
+  int32_t rr_q_raw_d;       // real row width (elements past it are zero, as prep's)
 };
 constexpr int kRrCap = 512;
 constexpr int kRrR0Cap = 64;
 constexpr int kRrMaxD = 512;   // widest f32 row the re-rank takes (wider: the split scan)
+constexpr int kRrRawRows = 16;  // query chunks up to which semantic lists take the raw-query path (no prep launch)
 constexpr uint32_t kRrSlow = 0xFFFFFFFFu;
 
 // Streaming top-K, second stage: per query, the exact top-K (full key order) of the
@@ -314,7 +336,7 @@ struct PrepArgs {
   float* eps_out;           // [Bpad]
   const float* istats;      // [3]: max |x̃−x|, max |x|, max |x̃| over the item rows
   float* h_out;             // [Bpad] int16 score-image quantum (rr_quantum; eps_out widened), or null
-  int32_t q_perm;           // 1: the bf16 operand in scan4 lane order (scan4_q_offset), not row-major
+  int32_t q_perm;           // the bf16 operand in lane order, not row-major: 1 = scan4's (scan4_q_offset), 2 = scan2's
 };
 
 struct MaskArgs {

@@ -140,23 +140,28 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   if (a.Mpad % bm || a.Ncols % bn || a.Kpad % bk || a.Mpad <= 0 || a.Ncols <= 0 || (a.slab_start & 31))
     return hipErrorInvalidValue;
   // the fused re-rank prologue lives in scan2 (bf16, query chunks of <= 128 rows) only
-  if (a.q_istats && (dtype != BF16 || scan4_used(BF16, a.Mpad) || !a.q_f32_out || !a.q_eps_out || a.cand))
+  if (a.q_istats && !a.q_raw && (dtype != BF16 || scan4_used(BF16, a.Mpad) || !a.q_f32_out || !a.q_eps_out || a.cand))
+    return hipErrorInvalidValue;
+  // the raw-query prologue: scan2 (bf16) with the list epilogue, raw f32 rows (d % 4 == 0)
+  if (a.q_raw && (dtype != BF16 || scan4_used(BF16, a.Mpad) || !a.lists || !a.q_src || a.q_ids || !a.q_istats ||
+                  !a.q_h_out || !a.q_eps_out || a.cand || a.q_d <= 0 || (a.q_d & 3) || a.q_d > a.Kpad || a.q_src_ld < a.q_d))
     return hipErrorInvalidValue;
   // the int16 score image: bf16 scans of rows up to kRrMaxD, slab epilogue only
   if (a.s_h && (dtype != BF16 || a.cand || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.Kpad > kRrMaxD))
     return hipErrorInvalidValue;
   // candidate lists: the bf16 scans of a re-rank search (rows up to kRrMaxD wide), periods of
   // at most kListMaxPeriod tiles covering every chunk
-  if (a.lists && (!a.s_h || a.q_istats || a.cand || a.l_period <= 0 || a.l_period > kListMaxPeriod || a.l_np <= 0 ||
+  if (a.lists && (!a.s_h || (a.q_istats && !a.q_raw) || a.cand || a.l_period <= 0 || a.l_period > kListMaxPeriod || a.l_np <= 0 ||
                   (int64_t)a.l_period * a.l_np * scan_chunks(BF16, a.Mpad, a.Ncols / 32, false) < a.Ncols / 32))
     return hipErrorInvalidValue;
   // the streaming pilot's top-m maxima: scan4 (bf16), slab mode, no other epilogue output
   if (a.pilot_top && (dtype != BF16 || !scan4_used(BF16, a.Mpad) || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.cand ||
                       a.lists || a.s_h || a.pilot_m != scan4_pilot_m(a.Kpad)))
     return hipErrorInvalidValue;
-  // the lane-order query operand is scan4's (prepped rows, no fused query prologue)
-  if (a.q_perm && (dtype != BF16 || !scan4_used(BF16, a.Mpad) || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.q_ids ||
-                   a.q_src))
+  // the lane-order query operand: scan4's (q_perm 1) or scan2's (2), prepped rows (no fused
+  // query prologue), bf16
+  if (a.q_perm && (dtype != BF16 || a.q_perm != (scan4_used(BF16, a.Mpad) ? 1 : 2) || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) ||
+                   a.q_ids || a.q_src || a.Kpad % 16))
     return hipErrorInvalidValue;
   if (gemm_uses_scan(dtype, a.Mpad, a.Kpad)) {
     if (dtype == BF16 ? launch_scan<uint16_t>(a, s) : launch_scan<float>(a, s)) return hipGetLastError();

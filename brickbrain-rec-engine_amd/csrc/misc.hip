@@ -2,6 +2,7 @@
 // union-blend), hard-constraint predicate masks and item-row conversion (gfx950).
 #include "common.h"
 #include "finalize_body.h"
+#include "qnorm.h"
 
 #include <cstdlib>
 
@@ -23,11 +24,7 @@ __device__ __forceinline__ void store_elem(void* p, int dtype, size_t i, float v
     ((float*)p)[i] = v;
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+__device__ __forceinline__ double wave_sum(double v) { return qn_wave_sum(v); }
 
 // ---------------------------------------------------------------------------------------
 // rows -> (optionally L2-normalised) rows of the index dtype, padded to Dpad.
@@ -195,7 +192,7 @@ __device__ __forceinline__ void load_chunk(const void* p, int dt, size_t sb, int
   }
 }
 
-constexpr int kPrepC = 8;  // rows up to 512 wide stay in registers (one load round)
+constexpr int kPrepC = kQnC;  // rows up to 512 wide stay in registers (one load round)
 
 // f32 -> three bf16 planes (x = xh + xm + xl exactly) for the split-precision scan
 
@@ -212,8 +209,9 @@ __device__ __forceinline__ void store_q(const PrepArgs& a, int row, int i, float
     o[0] = h;
     o[plane] = m;
     o[2 * plane] = l;
-  } else if (a.q_perm) {  // bf16 operand in scan4 lane order
-    ((uint16_t*)a.out)[scan4_q_offset(row, i >> 3, a.Dpad >> 4) * 8 + (i & 7)] = to_bf16(v);
+  } else if (a.q_perm) {  // bf16 operand in the scan's lane order
+    const size_t o = a.q_perm == 2 ? scan2_q_offset(row, i >> 3, a.Dpad >> 4) : scan4_q_offset(row, i >> 3, a.Dpad >> 4);
+    ((uint16_t*)a.out)[o * 8 + (i & 7)] = to_bf16(v);
   } else {
     store_elem(a.out, a.out_dtype, (size_t)row * a.Dpad + i, v);
   }
@@ -274,20 +272,12 @@ __device__ __forceinline__ void prep_rows(const PrepArgs& a, int blk) {
   if (a.Dpad <= 64 * kPrepC) {
     double x[kPrepC];
     load_chunk<kPrepC>(src, sdt, sb, 0, d, lane, x);
-    double norm = 1.0;
-    if (norm_on) {
-      double ss = 0.0;
-#pragma unroll
-      for (int c = 0; c < kPrepC; ++c) ss += x[c] * x[c];
-      ss = wave_sum(ss);
-      norm = sqrt(ss);
-      if (norm == 0.0) norm = 1.0;
-    }
+    const double norm = norm_on ? qn_norm(x) : 1.0;  // (qnorm.h: the list select's raw path shares it)
 #pragma unroll
     for (int c = 0; c < kPrepC; ++c) {
       const int i = lane + 64 * c;
       if (i < a.Dpad) {
-        const float v = (float)(x[c] / norm);
+        const float v = qn_elem(x[c], norm);
         store_q(a, row, i, v);
         if (a.out_f32) rr.add(a, row, i, v);
       }

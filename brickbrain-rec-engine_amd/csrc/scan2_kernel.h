@@ -134,20 +134,91 @@ __device__ __forceinline__ void scan2_rr_prologue(const GemmArgs& a, int q, int 
   }
 }
 
-// Query operand: 16-B chunk (2u + h) of this lane's query row into qf[u].
+// Raw-query re-rank prologue (GemmArgs.q_raw): lane half h of query row q holds elements
+// (2u + h)·8 .. +8 of the RAW f32 row, rounded to bf16 (RNE) — no normalisation and no
+// prep launch.  The code quantum of the list epilogue comes from the row's f32 sum of
+// squares n2 (the lane pair's two halves, added in either order: the same bits):
+//   Q = sqrt(n2·(1 + 2^-10)) >= ‖q‖       (f32 rounding of <= 512 squares)
+//   h = 2^-12·Q·(1 + 2^-8)·Ñ_x, rounded up  ->  |x̃·q̃| <= Ñ_x·‖q̃‖ <= 4096·h: codes fit 16 bits
+// Every workgroup derives the same h.  Those of item chunk 0 store it (q_h_out) and the
+// scan's error bound in raw units (q_eps_out), as prep's RrAcc but on the raw row:
+//   ε = E_x·‖q̃‖ + N_x·‖q̃ − q‖ + γ·Ñ_x·‖q̃‖          (f32 sums of squares scaled by 1 + 2^-10)
+//   ε' = (ε·(1+2^-20) + 1.01·h + Q·(N_x·(2^-23 + 2^-40) + 2^-20))·(1+2^-20)
+// where the Q term covers the exact score's own roundings (the normalised f32 row, the f64
+// sum rounded to f32) against x·q/‖q‖, scaled to raw units.
+template <int U>
+__device__ __forceinline__ float scan2_raw_prologue(const GemmArgs& a, int q, int h, bool write, uint4 (&qf)[U]) {
+  typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+  const float* row = (const float*)a.q_src + (size_t)q * a.q_src_ld;
+  const int d = a.q_d;
+  float n2 = 0.f, e2 = 0.f, b2 = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float4 v[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // (host: d % 4 == 0, 16-B aligned rows): clamp, load, select
+      const int k0 = (2 * u + h) * 8 + 4 * s;
+      const float4 t = *(const float4*)(row + (k0 < d ? k0 : d - 4));
+      v[s] = k0 < d ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      n2 = fmaf(v[s].x, v[s].x, n2);
+      n2 = fmaf(v[s].y, v[s].y, n2);
+      n2 = fmaf(v[s].z, v[s].z, n2);
+      n2 = fmaf(v[s].w, v[s].w, n2);
+    }
+    const bf2v b0 = {(__bf16)v[0].x, (__bf16)v[0].y}, b1 = {(__bf16)v[0].z, (__bf16)v[0].w};
+    const bf2v b2v = {(__bf16)v[1].x, (__bf16)v[1].y}, b3 = {(__bf16)v[1].z, (__bf16)v[1].w};
+    qf[u] = make_uint4(__builtin_bit_cast(uint32_t, b0), __builtin_bit_cast(uint32_t, b1),
+                       __builtin_bit_cast(uint32_t, b2v), __builtin_bit_cast(uint32_t, b3));
+    if (write) {  // (wave-uniform: the workgroups of item chunk 0)
+      const uint32_t w[4] = {qf[u].x, qf[u].y, qf[u].z, qf[u].w};
+      const float vv[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t ww = w[c >> 1];
+        const float bv = __uint_as_float((c & 1) ? (ww & 0xFFFF0000u) : (ww << 16));
+        const float e = vv[c] - bv;  // exact (bv is vv[c] rounded to 8 significant bits)
+        e2 = fmaf(e, e, e2);
+        b2 = fmaf(bv, bv, b2);
+      }
+    }
+  }
+  n2 += __shfl_xor(n2, 32);
+  const double Q = sqrt((double)n2 * (1.0 + 0x1p-10));
+  const float hq = __double2float_ru(0x1p-12 * Q * (1.0 + 0x1p-8) * (double)a.q_istats[2]);
+  if (write) {
+    e2 += __shfl_xor(e2, 32);
+    b2 += __shfl_xor(b2, 32);
+    if (h == 0) {
+      const double sc = 1.0 + 0x1p-10;
+      const double e = sqrt((double)e2 * sc), b = sqrt((double)b2 * sc);
+      const double ex = (double)a.q_istats[0], nx = (double)a.q_istats[1], nxb = (double)a.q_istats[2];
+      const double gam = 2.0 * (double)a.Kpad * 0x1p-24;
+      const double eps = ex * b + nx * e + gam * nxb * b;
+      const double ep = (eps * (1.0 + 0x1p-20) + 1.01 * (double)hq + Q * (nx * (0x1p-23 + 0x1p-40) + 0x1p-20)) *
+                        (1.0 + 0x1p-20);
+      a.q_h_out[q] = hq;
+      a.q_eps_out[q] = __double2float_ru(ep);
+    }
+  }
+  return hq;
+}
+
+// Query operand: 16-B chunk (2u + h) of this lane's query row into qf[u].  Returns the list
+// epilogue's code quantum of the raw-query prologue (0 otherwise: the epilogue reads s_h).
 template <typename T, int KU>
-__device__ __forceinline__ void scan2_load_queries(const GemmArgs& a, int q, int h, uint4 (&qf)[KU / 2],
-                                                   bool rr_write = false) {
+__device__ __forceinline__ float scan2_load_queries(const GemmArgs& a, int q, int h, uint4 (&qf)[KU / 2],
+                                                    bool rr_write = false) {
   constexpr int U = KU / 2;
   if (q >= a.M_valid) {
 #pragma unroll
     for (int u = 0; u < U; ++u) qf[u] = make_uint4(0, 0, 0, 0);
-    return;
+    return 0.f;
   }
   if constexpr (sizeof(T) == 2 && KU <= kRrMaxD / 8) {
+    if (a.q_raw) return scan2_raw_prologue<U>(a, q, h, rr_write, qf);
     if (a.q_istats) {  // exact re-rank operands (GemmArgs.q_f32_out)
       scan2_rr_prologue<U>(a, q, h, rr_write, qf);
-      return;
+      return 0.f;
     }
   }
   if (a.q_ids) {  // similar / hybrid: the stored (normalised, padded) item row of the liked set
@@ -159,7 +230,7 @@ __device__ __forceinline__ void scan2_load_queries(const GemmArgs& a, int q, int
       const uint4 v = *(const uint4*)(row + (2 * u + h) * 16);
       qf[u] = ok ? v : make_uint4(0, 0, 0, 0);
     }
-    return;
+    return 0.f;
   }
   if (a.q_src) {  // raw f32 rows (T == float): normalise here
     const float* row = (const float*)a.q_src + (size_t)q * a.q_src_ld;
@@ -198,11 +269,18 @@ __device__ __forceinline__ void scan2_load_queries(const GemmArgs& a, int q, int
     for (int u = 0; u < U; ++u)
       qf[u] = make_uint4(__float_as_uint(x[u].x), __float_as_uint(x[u].y), __float_as_uint(x[u].z),
                          __float_as_uint(x[u].w));
-    return;
+    return 0.f;
+  }
+  if (sizeof(T) == 2 && a.q_perm) {  // lane-order operand (scan2_q_offset): 1 KiB per wave load
+    const uint4* qp = (const uint4*)a.Q + scan2_q_offset(q, h, U);
+#pragma unroll
+    for (int u = 0; u < U; ++u) qf[u] = qp[(size_t)u * 64];
+    return 0.f;
   }
   const char* qrow = (const char*)a.Q + (size_t)q * a.ldq * sizeof(T);
 #pragma unroll
   for (int u = 0; u < U; ++u) qf[u] = *(const uint4*)(qrow + (2 * u + h) * 16);
+  return 0.f;
 }
 
 // Per-lane half-tile maxima of one 32-item tile (this lane's 16 items): te over eligible
@@ -348,7 +426,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   if (tile_lo >= tile_hi) return;  // uniform per workgroup
 
   uint4 qf[U];
-  scan2_load_queries<T, KU>(a, q, h, qf, chunk == 0 && a.q_istats != nullptr);
+  const float hq_raw = scan2_load_queries<T, KU>(a, q, h, qf, chunk == 0 && a.q_istats != nullptr);
   float qa[sizeof(T) == 4 ? 4 * U : 1];  // f32: the operand as 4U scalars, pinned to AGPRs
   if constexpr (sizeof(T) == 4) {
 #pragma unroll
@@ -418,7 +496,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   constexpr bool LIST = (ABL & kScanList) != 0 && !STREAM && !S16;
   float k2 = 0.f;
   if constexpr (LIST) {
-    const float hq = q < a.M_valid ? a.s_h[q] : 0.f;
+    const float hq = a.q_raw ? hq_raw : q < a.M_valid ? a.s_h[q] : 0.f;
     k2 = hq > 0.f ? 1.0f / (hq * 65535.f) : 0.f;
     asm volatile("" : "+v"(k2));  // consumed before any LDS-DMA is in flight
   }

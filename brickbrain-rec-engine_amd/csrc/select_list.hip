@@ -27,6 +27,7 @@
 // every eligible item of the row (slow, never taken on distinct data; tests drive it).
 #include "common.h"
 #include "list_epi.h"
+#include "qnorm.h"
 #include "select_util.h"
 
 namespace bb {
@@ -102,9 +103,11 @@ __device__ __forceinline__ void ls_append(const uint32_t* seg, int ns, uint64_t*
 }
 
 // The rescore of the list select: 32 rows in flight per workgroup at d = 384, the query
-// chunks re-read from LDS each round — the kernel fits 170 VGPRs, three workgroups per CU
-// (the hybrid select runs 2·B of them; the gathers are bound by the chip's bandwidth, not by
-// rows in flight).
+// chunks re-read from LDS each round — the kernel fits 138 VGPRs, three workgroups per CU
+// (the hybrid select runs 2·B of them).  The gathers are bound by the chip's bandwidth, not
+// by rows in flight: at configs[1] 256 rows x ~90 candidates x 1.5 KB = 36 MB in ~6 us, and
+// 3 us with every row gathering the same (cache-resident) item (r03_ab); 96 rows in flight
+// (one round) measured no faster (r03_w).
 __device__ __forceinline__ void ls_rescore(uint64_t* keys, int m, const SelectArgs& a, const float* qs) {
   const int cpl = ((a.rr_d >> 2) + 15) >> 4;
   const int t = threadIdx.x;
@@ -124,7 +127,6 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   uint32_t* r0s = (uint32_t*)(dsm + kLsOffR0);
   float* qs = (float*)(dsm + kLsOffQs);
   uint32_t* misc = (uint32_t*)(dsm + kLsOffMisc);
-  uint32_t* scan_sh = (uint32_t*)(dsm + kLsOffScan);
   uint32_t* allseg = (uint32_t*)(dsm + kLsOffAll);  // both halves of every tile
   uint32_t* allpre = allseg + 4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -150,11 +152,23 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     allpre[2] = (uint32_t)T * 32;
   }
   const int nq4 = a.rr_d >> 2;
-  if (tid < nq4) ((float4*)qs)[tid] = ((const float4*)(a.rr_q + (size_t)row * a.rr_ld))[tid];
-
-  // Δ: the re-rank margin in codes (h = 0: a zero query row, every code equal -> take all)
   const float hq = a.s_h[row];
-  const uint32_t delta = hq > 0.f ? (uint32_t)fminf(ceilf(rr_margin(a.rr_eps[row]) / hq), 60000.f) + 2u : 0x10000u;
+  // raw-query lists (GemmArgs.q_raw): wave 0 loads the raw row now and normalises it into
+  // the LDS query after the classification (prep_kernel's arithmetic, qnorm.h: the same f32
+  // row bit for bit), so its latency hides under the bound search
+  float xq[kQnC];
+  if (a.rr_q_raw) {
+    if (wave == 0) {
+      const float* qr = a.rr_q_raw + (size_t)row * a.rr_q_raw_ld;
+#pragma unroll
+      for (int c = 0; c < kQnC; ++c) {
+        const int i = lane + 64 * c;
+        xq[c] = i < a.rr_q_raw_d ? qr[i] : 0.f;
+      }
+    }
+  } else if (tid < nq4) {
+    ((float4*)qs)[tid] = ((const float4*)(a.rr_q + (size_t)row * a.rr_ld))[tid];
+  }
 
   // ---- lists of this row: thread t holds lists t, t + 256, ... ----
   constexpr int kLPT = kLsMaxLists / kSelectThreads;
@@ -187,6 +201,8 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   }
   __syncthreads();  // hist and misc cleared
   stamp(1);
+  // Δ: the re-rank margin in codes (h = 0: a zero query row, every code equal -> take all)
+  const uint32_t delta = hq > 0.f ? (uint32_t)fminf(ceilf(rr_margin(a.rr_eps[row]) / hq), 60000.f) + 2u : 0x10000u;
 
   // ---- bound: T0 = K-th largest code over every list key, by a bitwise search: each wave
   // counts its lanes' keys >= c with ballots, the four wave counts meet in LDS (two
@@ -314,6 +330,17 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
         r0s[2 * s] = whole ? (uint32_t)tlo : (uint32_t)(tlo + (rv[i].x & 0xFFFFu));
         r0s[2 * s + 1] = ((uint32_t)nt << 1) | (uint32_t)hh;
       }
+    }
+  }
+  if (a.rr_q_raw && wave == 0) {
+    double xd[kQnC];
+#pragma unroll
+    for (int c = 0; c < kQnC; ++c) xd[c] = (double)xq[c];
+    const double nrm = qn_norm(xd);
+#pragma unroll
+    for (int c = 0; c < kQnC; ++c) {
+      const int i = lane + 64 * c;
+      if (i < a.rr_d) qs[i] = qn_elem(xd[c], nrm);
     }
   }
   __syncthreads();
@@ -518,10 +545,12 @@ __global__ __launch_bounds__(kSelectThreads) __attribute__((amdgpu_waves_per_eu(
   else
     select_list_body(a1, xcd_row(blockIdx.x - B, B));
 }
-
 static bool list_args_ok(const SelectArgs& a) {
   const int L = 2 * a.l_chunks * a.l_np;
-  return a.lists && a.rr_eps && a.s_h && a.rr_x && a.rr_q && a.rr_d > 0 && a.rr_d <= kRrMaxD && !(a.rr_d & 3) &&
+  return a.lists && a.s_h && a.rr_x && a.rr_d > 0 && a.rr_d <= kRrMaxD && !(a.rr_d & 3) &&
+         a.rr_eps && (a.rr_q_raw ? a.rr_q_raw_d > 0 && a.rr_q_raw_d <= a.rr_d && a.rr_q_raw_ld >= a.rr_q_raw_d &&
+                                       !a.max_inout
+                                     : a.rr_q != nullptr) &&
          a.K > 0 && a.K <= kMaxKInt && a.n_cols > 0 && a.l_chunks > 0 && a.l_np > 0 && a.l_period > 0 &&
          L <= kLsMaxLists && 2 * a.l_chunks <= 2 * kSelectThreads && a.l_tiles * 32 >= a.n_cols &&
          (a.l_tiles + a.l_chunks - 1) / a.l_chunks <= 2047 && !(a.slab_start & 31) && !a.carry_in &&

@@ -346,7 +346,7 @@ __device__ __forceinline__ void rescore_rows(uint64_t* keys, int m, const Select
       // branch-free (a clamped re-read of the last key): a conditional read splits the
       // rows into blocks of their own and leaves one row's loads in flight at a time
       gid[u] = gid_of(keys[min(c0 + u, m - 1)]);
-      const f4v* xr = (const f4v*)(a.rr_x + (size_t)(gid[u] - a.rr_gid_base) * a.rr_ld);
+      const f4v* xr = (const f4v*)(a.rr_x + (a.ablate & 1 ? (size_t)0 : (size_t)(gid[u] - a.rr_gid_base) * a.rr_ld));
 #pragma unroll
       for (int j = 0; j < CPL; ++j) xv[u][j] = xr[min(p + 16 * j, nch - 1)];
     }
