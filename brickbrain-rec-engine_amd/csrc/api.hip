@@ -655,8 +655,13 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   const int64_t ws = stream && !x->ws_set ? std::max<int64_t>(x->ws_cap, 4ll << 30) : x->ws_cap;
   int64_t n0 = 0, lds, Bc;
   if (stream) {
+    // pilot rows: n/16, or n/8 below the two-level bound's range (< 500K rows) for batches of
+    // 256+, where the candidate select dominates: 125K x 768, B = 4096 appends ~K_int·n/n0
+    // keys per query, and T(n0) ≈ pilot + select is minimal near n/8 (BB_PILOT_DIV, A/B runs)
+    static const int pilot_div_env = ab_env("BB_PILOT_DIV") ? atoi(ab_env("BB_PILOT_DIV")) : 0;
+    const int64_t pilot_div = pilot_div_env > 0 ? pilot_div_env : (x->n < 500000 && B >= 256 ? 8 : 16);
     const int64_t n0_target =
-        std::min<int64_t>(round_up(std::max<int64_t>(x->n / 16, 64ll * K_int), kTileRows), x->Npad);
+        std::min<int64_t>(round_up(std::max<int64_t>(x->n / pilot_div, 64ll * K_int), kTileRows), x->Npad);
     const int64_t n0_min = std::min<int64_t>(n0_target, 8192);
     Bc = std::min<int64_t>(pad_rows(B), 8192);
     while (Bc > rq && Bc * n0_min * 4 > ws) Bc = std::max<int64_t>(rq, Bc / 2 / rq * rq);
