@@ -561,12 +561,64 @@ __global__ __launch_bounds__(256) void pilot_bound_kernel(const uint32_t* top, i
   if (tid == 0) thr_out[row] = (uint64_t)P << 32;
 }
 
+// The same bound with one wave per row (four rows per workgroup) when a row has at most
+// 1,024 values (every configs[3]/[4] geometry: 2·chunks·m = 128): the search needs no
+// barrier at all (the workgroup version paid one per bit for 4,096 short workgroups).
+__global__ __launch_bounds__(256) void pilot_bound_wave_kernel(const uint32_t* top, int n_chunks, int m, int nb, int K,
+                                                               int B, uint64_t* thr_out) {
+  constexpr int kPer = 16;  // values per lane: 2·n_chunks·m <= 1024
+  const int lane = threadIdx.x & 63, row = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (row >= B) return;  // (whole waves)
+  const int blk = row >> 5, r = row & 31;
+  const int nv = 2 * n_chunks * m;
+  uint32_t v[kPer];
+  uint32_t hi = 0, lo = 0xFFFFFFFFu, cnt = 0;
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int j = lane + e * 64;
+    uint32_t x = 0;
+    if (j < nv) {
+      const int i = j % m, ch = j / m, c = ch >> 1, hh = ch & 1;
+      x = top[((size_t)(c * nb + blk) * 64 + hh * 32 + r) * m + i];
+    }
+    v[e] = x;
+    hi = max(hi, x);
+    lo = x ? min(lo, x) : lo;
+  }
+  auto count_ge = [&](uint32_t c) -> uint32_t {
+    uint32_t n = 0;
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) n += (uint32_t)__popcll(__ballot(v[e] >= c));
+    return n;
+  };
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+    lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+  }
+  cnt = count_ge(1u);
+  uint32_t P = 0;  // 0 = fewer than K values: take every eligible item
+  if (cnt >= (uint32_t)K) {
+    const uint32_t d = hi ^ lo;
+    const int top_bit = d ? 31 - __builtin_clz(d) : -1;
+    P = top_bit < 0 ? hi : hi & ~((2u << top_bit) - 1u);
+    for (int bit = top_bit; bit >= 0; --bit) {
+      const uint32_t c = P | (1u << bit);
+      if (count_ge(c) >= (uint32_t)K) P = c;
+    }
+  }
+  if (lane == 0) thr_out[row] = (uint64_t)P << 32;
+}
+
 hipError_t launch_pilot_bound(const uint32_t* top, int n_chunks, int m, int nb, int K, int B, uint64_t* thr_out,
                               hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (!top || !thr_out || n_chunks <= 0 || m <= 0 || 2 * n_chunks * m > 16 * 256 || K <= 0 || B > 32 * nb)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pilot_bound_kernel, dim3(B), dim3(256), 0, s, top, n_chunks, m, nb, K, thr_out);
+  if (2 * n_chunks * m <= 16 * 64)
+    hipLaunchKernelGGL(pilot_bound_wave_kernel, dim3((B + 3) / 4), dim3(256), 0, s, top, n_chunks, m, nb, K, B, thr_out);
+  else
+    hipLaunchKernelGGL(pilot_bound_kernel, dim3(B), dim3(256), 0, s, top, n_chunks, m, nb, K, thr_out);
   return hipGetLastError();
 }
 
