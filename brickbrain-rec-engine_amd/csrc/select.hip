@@ -733,13 +733,70 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
       if (e < min(nw, a.K)) sel[off + e] = v[s8];
     }
     __syncthreads();
-    if (wave != 0) return;
-    int m = 0;
-    for (int w = 0; w < kSelectThreads / 64; ++w) m += min(min(max(n - w * 512, 0), 512), a.K);
-    if (m <= 64) wave_sort_emit<1>(sel, m, sa, row, drop);
-    else if (m <= 128) wave_sort_emit<2>(sel, m, sa, row, drop);
-    else if (m <= 256) wave_sort_emit<4>(sel, m, sa, row, drop);
-    else wave_sort_emit<8>(sel, m, sa, row, drop);
+    // merge the four sorted segments by rank: a key's output position is its position in
+    // its own segment plus the keys above it in the other three (binary searches; keys are
+    // distinct) — every thread emits its own keys, no second sort
+    int seg_off[kSelectThreads / 64 + 1], m = 0;
+#pragma unroll
+    for (int w = 0; w < kSelectThreads / 64; ++w) {
+      seg_off[w] = m;
+      m += min(min(max(n - w * 512, 0), 512), a.K);
+    }
+    seg_off[kSelectThreads / 64] = m;
+    uint64_t mk[2];
+    int rk[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int i = tid + e * kSelectThreads;
+      mk[e] = i < m ? sel[i] : 0ull;
+      rk[e] = 0;
+      if (i >= m) continue;
+#pragma unroll
+      for (int w = 0; w < kSelectThreads / 64; ++w) {
+        const int b = seg_off[w], L = seg_off[w + 1] - b;
+        if (i >= b && i < b + L) {
+          rk[e] += i - b;
+          continue;
+        }
+        int lo = 0, hi = L;  // keys of segment w above mk: the first index below it
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (sel[b + mid] > mk[e]) lo = mid + 1;
+          else hi = mid;
+        }
+        rk[e] += lo;
+      }
+    }
+    uint64_t* head = red;  // the rank-0 key (red[0..3] were consumed above)
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+      if (tid + e * kSelectThreads < m && rk[e] == 0) *head = mk[e];
+    __syncthreads();
+    if (sa.out_scores) {
+      const int start = (drop && m && *head == drop) ? 1 : 0;
+      const int c = min(sa.k_final, m - start);
+      float* sc = sa.out_scores + (size_t)row * sa.k_final;
+      int64_t* id = sa.out_ids + (size_t)row * sa.k_final;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int pos = rk[e] - start;
+        if (tid + e * kSelectThreads < m && pos >= 0 && pos < c) {
+          sc[pos] = float_of_ord(ordk_of(mk[e]));
+          id[pos] = (int64_t)gid_of(mk[e]);
+        }
+      }
+      for (int i = c + tid; i < sa.k_final; i += kSelectThreads) {
+        sc[i] = 0.f;
+        id[i] = -1;
+      }
+      if (sa.out_counts && tid == 0) sa.out_counts[row] = c;
+      return;
+    }
+    uint64_t* out = sa.keys_out + (size_t)row * sa.K;
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+      if (tid + e * kSelectThreads < m && rk[e] < sa.K) out[rk[e]] = mk[e];
+    for (int i = m + tid; i < sa.K; i += kSelectThreads) out[i] = 0ull;
     return;
   }
   // more than 256: the K-th largest key, then the keys >= it (exactly min(K, n) of them)
