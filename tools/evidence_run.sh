@@ -1,6 +1,6 @@
 # Final-evidence pass: bench.py line (with cpu_baseline) and rocprofv3 --kernel-trace --stats per workload.
 set -e
-O=gpurun_out/r03h; mkdir -p $O
+O=gpurun_out/${1:-r03h}; mkdir -p $O
 R=$(pwd)
 for w in c2 c3 c4 c5; do
   st=""
