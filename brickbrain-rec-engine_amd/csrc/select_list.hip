@@ -535,14 +535,15 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   for (int i = tid; i < K; i += kSelectThreads) out[i] = sel[i];
 }
 
-__global__ __launch_bounds__(kSelectThreads) __attribute__((amdgpu_waves_per_eu(3))) void select_list_kernel(SelectArgs a, int B) {
+__global__ __launch_bounds__(kSelectThreads) __attribute__((amdgpu_waves_per_eu(4))) void select_list_kernel(SelectArgs a, int B) {
   select_list_body(a, xcd_row(blockIdx.x, B));
 }
 // both sides of a hybrid search: workgroups [0, B) side 0, the rest side 1.  Four workgroups
 // per CU (128 VGPRs, 44 B/lane of spills outside the rescore loop): configs[2]'s 2·B = 2,048
 // workgroups run in two full rounds instead of 2.67 — 50.4 -> 41.1 us per batch, 10.76 ->
-// 11.45 M q/s (r03j).  Five per CU (96 VGPRs, 176 B/lane spilled) is slower (55 us); the
-// single-side kernel at four per CU gains nothing at configs[1] (B = 256: one round either way).
+// 11.45 M q/s (r03j).  Five per CU (96 VGPRs, 176 B/lane spilled) is slower (55 us).  The
+// single-side kernel above runs at four per CU too: neutral at configs[1] (B = 256 is one
+// round either way), select 36.4 -> 32.3 us at B = 1024 and 99.8 -> 94.6 us at 4096 (r03m).
 __global__ __launch_bounds__(kSelectThreads) __attribute__((amdgpu_waves_per_eu(4))) void select_list_dual_kernel(SelectArgs a0, SelectArgs a1, int B) {
   if ((int)blockIdx.x < B)
     select_list_body(a0, xcd_row(blockIdx.x, B));
