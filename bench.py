@@ -74,7 +74,7 @@ def scan_kernel_info(dtype, width, batch):
 
 
 def roofline(flops_alg, bytes_alg, kernel_us, dtype, kname, mfma_per_flop, traffic):
-    """Roofline object of the dominant kernel.  The binding ceiling follows SURVEY.md §8(d):
+    """Roofline object of one kernel.  The binding ceiling follows SURVEY.md §8(d):
     max(issued MFMA flops / MFMA peak, algorithmic bytes / HBM peak).  `achieved` is the
     binding side's rate: issued MFMA TFLOP/s (algorithmic flops × MFMA flops per algorithmic
     flop) against the dense peak of the issued instruction, or algorithmic GB/s against HBM;
@@ -105,6 +105,39 @@ def roofline(flops_alg, bytes_alg, kernel_us, dtype, kname, mfma_per_flop, traff
     return out
 
 
+def family_kernels(workload, dtype, B, scan_name):
+    """Kernel behind each profiling family of bb_get_profile (HIP events on the launch stream)."""
+    if workload == "c2" and dtype == "f32" and B <= 16:
+        return {"gemm": "sq_scan_kernel (one exact f32/f64 pass, small batch)", "select": "sq_merge_kernel"}
+    if workload == "c3":
+        return {"prep": "prep2_kernel", "gemm": scan_name, "select": "select_list_dual_kernel",
+                "finalize": "finalize1_kernel"}
+    return {"prep": "prep_kernel", "gemm": scan_name,
+            "select": "select_list_kernel" if dtype == "f32" else "select_kernel", "rerank": "rerank_kernel",
+            "finalize": "finalize1_kernel"}
+
+
+def dominant_roofline(fam_us, names, flops, alg_bytes, step_us, dtype, scan_mpf, pmc_key):
+    """roofline object for the kernel family that takes the most device time per step (HIP
+    events, bb_get_profile), with SURVEY.md §8(d)'s algorithmic work of one search priced
+    against that kernel's time; `step` prices the same work against the whole step (wall time
+    per step of the timed window), `scan` reports the scan launch's own MFMA / HBM rates."""
+    dom = max(fam_us, key=fam_us.get)
+    kname = names.get(dom, dom)
+    mpf = scan_mpf if dom == "gemm" else 1.0
+    out = roofline(flops, alg_bytes, fam_us[dom], dtype, kname, mpf, load_pmc(pmc_key, dom))
+    out["family"] = dom
+    out["step"] = {"us": round(step_us, 3), "achieved_gbs": round(alg_bytes / (step_us * 1e-6) / 1e9, 1),
+                   "frac": round(alg_bytes / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                   "note": "algorithmic bytes of one search / wall time per step of the timed window"}
+    if "gemm" in fam_us:
+        sc = roofline(flops, alg_bytes, fam_us["gemm"], dtype, names.get("gemm", "gemm"), scan_mpf,
+                      load_pmc(pmc_key, "gemm"))
+        out["scan"] = {k: sc[k] for k in ("kernel", "kernel_us", "mfma_issued_tflops", "mfma_frac",
+                                          "hbm_frac_at_alg_bytes", "traffic")}
+    return out
+
+
 def unit_rows_torch(n, d, seed, device, chunk=1 << 20):
     import torch
     g = torch.Generator(device=device)
@@ -116,13 +149,14 @@ def unit_rows_torch(n, d, seed, device, chunk=1 << 20):
     return out
 
 
-def load_pmc(key):
-    """HBM bytes per dominant-kernel launch from the committed rocprofv3 PMC summary."""
+def load_pmc(key, family="gemm"):
+    """HBM bytes per step of one kernel family from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, tools/pmc_traffic.py), or None when not collected."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        e = d.get(key, {}).get("gemm")
+        e = d.get(key, {}).get(family)
         return None if e is None else float(e["hbm_bytes_per_launch"])
     except Exception:
         return None
@@ -159,6 +193,7 @@ def cpu_baseline(x_np, q_np, k, budget_s=8.0, sweep_s=2.0):
     ids0 = batched_cosine_topk(x_np, q_np, k)[0]
     nb, el, lat = _time_cpu(lambda: batched_cosine_topk(x_np, q_np, k), budget_s, 400)
     out = {"value": round(nb * B / el, 1), "unit": "queries/s", "cores": int(cores), "kind": "port",
+           "rank": 0,
            "p50_ms": round(1e3 * float(np.median(lat)), 3),
            "sample": f"{nb} batches x {B} queries x {x_np.shape[0]} x {x_np.shape[1]} fp32 (numpy/BLAS restatement, "
                      f"oracle/restatement.py batched_cosine_topk), timed"}
@@ -169,7 +204,7 @@ def cpu_baseline(x_np, q_np, k, budget_s=8.0, sweep_s=2.0):
         from threadpoolctl import threadpool_limits
     except Exception:
         threadpool_limits = None
-    for threads in (cores, 1):
+    for threads in ((cores, 1) if sweep_s > 0 else ()):
         for b, kk in ((1, 10), (256, 50), (1024, 50), (4096, 50)):
             qb = qs[:b]
 
@@ -424,6 +459,60 @@ def gpu_batch_sweep(brickrec, base, local, dev, seconds=0.5):
     return res
 
 
+def launch_ranks(args):
+    """`--gpus N` without a launcher: start the N rank processes (torch.distributed.run on
+    127.0.0.1, one rank per GPU) as a child before this process touches any GPU, and return
+    its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def dry_run(args):
+    """Device-free rehearsal (tests/test_bench_launcher.py): the ranks join a gloo group, run
+    the timed region's barriers and max-over-ranks reduction around a no-op step, and rank 0
+    times the CPU baseline on a small sample and prints the line.  Nothing is measured on a
+    GPU: value is null."""
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out = {"metric": "similarity queries/sec + p50 latency, 384-d x 25,216 items (configs[1])", "value": None,
+           "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+           "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": args.dtype, "data": "synthetic", "max_rank_s": float(t.item()),
+           "config": {"workload": "dry run (no device)", "parallelism": f"replicas x{world}" if world > 1 else "single"},
+           "roofline": None, "cpu_baseline": None}
+    if rank == 0 and not args.no_cpu:
+        from oracle.restatement import unit_rows
+        x_np = unit_rows(4096, DIM, 1234)
+        q_np = unit_rows(BATCH, DIM, 4321)
+        out["cpu_baseline"], _ = cpu_baseline(x_np, q_np, TOPK, budget_s=args.cpu_budget, sweep_s=0.0)
+        out["cpu_baseline"]["sample"] += " (dry run: 4,096 rows)"
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -437,7 +526,14 @@ def main():
     ap.add_argument("--lane-copies", action="store_true", help="one uploaded copy of the rows per in-flight lane")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2 = configs[1] (default line); c3 = configs[2] hybrid; c4 / c5 = the sharded configs[3] / [4]")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="device-free rehearsal of the launcher and the reporting path (gloo ranks, no GPU)")
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU-baseline timing")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
+    if args.dry_run:
+        return dry_run(args)
 
     import torch
     import torch.distributed as dist
@@ -447,7 +543,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=dev)   # RCCL
+        world = dist.get_world_size()                    # n_gpus = the ranks that joined
     if args.workload in SHARDED:
         return run_sharded(args, rank, world, local, dev)
 
@@ -510,15 +607,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
 
-    # ---- per-kernel device time (HIP events on the launch stream), same K steps ----
+    # ---- per-kernel device time (HIP events on the launch stream), same K steps, one batch
+    # at a time (lane 0 alone: kernel averages not inflated by the other lanes' batches) ----
     idx.set_profiling(True)
     for _ in range(args.steps):
         run()
     prof = idx.profile()
     idx.set_profiling(False)
-    g = prof["gemm"]
-    # all scan launches of one step (hybrid: the content and CF sides), per step
-    gemm_us = 1e3 * g["ms"] / max(args.steps, 1)
+    fam_us = {k: 1e3 * v["ms"] / max(args.steps, 1) for k, v in prof.items() if v["launches"]}
     es = 4 if args.dtype == "f32" else 2
     if hybrid:
         r = 50
@@ -529,13 +625,14 @@ def main():
         if args.dtype == "f32" and not (ab and os.environ.get("BB_NO_RR")) and not (ab and os.environ.get("BB_DUAL") == "0"):
             kname = ("scan4_dual_kernel<48,8,list> (content d=384 + CF r=50 one-product bf16 scans in one launch, "
                      "bounded per-lane candidate lists; exact f32 re-rank of the candidates in the list select)")
-        kname = "scan launches of one hybrid step (content d=384 + CF r=50): " + kname
     else:
         flops = 2.0 * B * N_ITEMS * DIM
         alg_bytes = N_ITEMS * DIM * es + B * DIM * 4 + B * TOPK * 8    # items + queries + top-K out
         kname, mpf = scan_kernel_info(args.dtype, DIM, B)
     pmc_key = "c3" if hybrid else args.dtype
-    roof = roofline(flops, alg_bytes, gemm_us, args.dtype, kname, mpf, load_pmc(pmc_key))
+    step_us = 1e6 * el / args.steps
+    roof = dominant_roofline(fam_us, family_kernels(args.workload, args.dtype, B, kname), flops, alg_bytes, step_us,
+                             args.dtype, mpf, pmc_key)
 
     # ---- MALL-cold latency (256 MiB Infinity Cache flushed before each step) ----
     flush = torch.empty(640 << 20, dtype=torch.uint8, device=dev)
@@ -578,23 +675,23 @@ def main():
                    "parallelism": f"replicas x{world}" if world > 1 else "single",
                    "inflight_batches": args.inflight},
         "roofline": roof,
-        "kernels_us_per_step": {k: round(1e3 * v["ms"] / max(args.steps, 1), 3) for k, v in prof.items()
-                                if v["launches"]},
+        "kernels_us_per_step": {k: round(v, 3) for k, v in fam_us.items()},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_sweep and not hybrid:
         out["gpu_batch_sweep"] = gpu_batch_sweep(brickrec, base, local, dev)
-    if rank == 0 and world == 1 and not args.no_cpu and hybrid:
+    # rank 0 times the CPU baseline on every line (replicas: the same per-rank workload)
+    if rank == 0 and not args.no_cpu and hybrid:
         x_np = x.cpu().numpy()
         cb, ids0 = cpu_baseline_hybrid(x_np, extra["f"], q["mask"], q["liked"], q["rated"], q["u"], TOPK)
         gpu_ids = o_ids.cpu().numpy()
         cb["topk_set_agreement_with_gpu"] = round(float(np.mean([set(gpu_ids[i][gpu_ids[i] >= 0]) == set(ids0[i])
                                                                  for i in range(len(ids0))])), 4)
         out["cpu_baseline"] = cb
-    if rank == 0 and world == 1 and not args.no_cpu and not hybrid:
+    if rank == 0 and not args.no_cpu and not hybrid:
         x_np = x.cpu().numpy()
         q_np = q.cpu().numpy()
-        cb, ids0 = cpu_baseline(x_np, q_np, TOPK)
+        cb, ids0 = cpu_baseline(x_np, q_np, TOPK, budget_s=args.cpu_budget)
         gpu_ids = o_ids.cpu().numpy()
         same = float(np.mean([set(gpu_ids[i]) == set(ids0[i]) for i in range(B)]))
         cb["topk_set_agreement_with_gpu"] = round(same, 4)
@@ -606,4 +703,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

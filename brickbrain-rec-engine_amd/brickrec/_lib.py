@@ -19,6 +19,7 @@ BB_MODE_SEMANTIC, BB_MODE_SIMILAR, BB_MODE_CF, BB_MODE_HYBRID = 0, 1, 2, 3
 BB_Q_OUT_KEYS = 1
 BB_Q_NULL_STREAM = 2
 BB_OPT_STREAM, BB_OPT_STREAM_MIN_ITEMS, BB_OPT_WORKSPACE_BYTES, BB_OPT_STREAM_REFINE, BB_OPT_RR_LISTS = 1, 2, 3, 4, 5
+BB_OPT_SMALL_BATCH = 6
 BB_OK, BB_E_ARG, BB_E_HIP, BB_E_STATE, BB_E_NOMEM = 0, -1, -2, -3, -4
 
 # every entry point include/brickrec.h declares (checked by tests/test_abi.py)

@@ -137,11 +137,18 @@ class ShardedIndex:
         """Per-query exclusions (CF: the user's rated sets, recommendation_system.py:441-451) as
         a device bitset [B, words] of this rank's rows, scattered on the device from global item
         ids: a list of B id arrays, or an int64 tensor [B, m] padded with -1.  Ids outside
-        [lo, hi) belong to other ranks and are dropped here; ids within a row must be unique."""
+        [lo, hi) belong to other ranks and are dropped here; repeated ids count once."""
         import torch
         dev = self._device()
         if isinstance(item_ids, torch.Tensor):
             ids = item_ids.to(dev, torch.int64)
+            if ids.dim() != 2:
+                raise ValueError("excl_bits: an id tensor must be [B, m] (pad with -1)")
+            # one bit per distinct id: sort each row and drop repeats (the scatter below adds)
+            ids, _ = torch.sort(ids, dim=1)
+            rep = torch.zeros_like(ids, dtype=torch.bool)
+            rep[:, 1:] = ids[:, 1:] == ids[:, :-1]
+            ids = ids.masked_fill(rep, -1)
         else:
             lists = [np.unique(np.asarray(r, np.int64)) for r in item_ids]
             m = max([len(r) for r in lists] + [1])
@@ -155,22 +162,38 @@ class ShardedIndex:
         ok = (ids >= 0) & (loc >= 0) & (loc < self.n_local)
         rowi = torch.arange(B, device=dev).unsqueeze(1).expand_as(ids)
         word = (rowi * max(W, 1) + (loc >> 5))[ok]
-        flat.index_add_(0, word, torch.ones_like(word) << (loc[ok] & 31))   # unique ids: sum == or
+        flat.index_add_(0, word, torch.ones_like(word) << (loc[ok] & 31))   # distinct ids: sum == or
         flat = (flat + (1 << 31)) % (1 << 32) - (1 << 31)                  # u32 words as int32
         return flat.to(torch.int32).view(B, max(W, 1))[:, :W].contiguous()
 
     def _local_bits(self, a, rows: bool):
-        """A search argument as this rank's device bitset: per-rank int32 words pass through;
-        a global bool host array (small cases) is sliced and packed."""
+        """A search argument as this rank's device bitset.  Packed words (int32 / uint32, numpy
+        or torch) must already be this rank's: shape (words,) for a mask, (B, words) for the
+        per-query exclusions — anything else raises (a global or another rank's bitset would
+        hand the kernel a buffer of the wrong length).  Bool arrays (global [.., N] or local
+        [.., n_local]) are sliced and packed here."""
         import torch
         if a is None:
             return None
-        if isinstance(a, torch.Tensor) and a.dtype == torch.int32 and a.shape[-1] == self.words:
-            return a.to(self._device())
-        from .engine import bits_from_bool
-        g = np.asarray(a.cpu() if isinstance(a, torch.Tensor) else a, bool)
-        loc = g[..., self.lo:self.hi] if g.shape[-1] == self.n else g
-        return torch.as_tensor(bits_from_bool(loc).view(np.int32)).to(self._device())
+        ndim = 2 if rows else 1
+        is_t = isinstance(a, torch.Tensor)
+        dt = a.dtype
+        if (is_t and dt == torch.bool) or (not is_t and np.asarray(a).dtype == np.bool_):
+            from .engine import bits_from_bool
+            g = np.asarray(a.cpu() if is_t else a, bool)
+            if g.ndim != ndim or g.shape[-1] not in (self.n, self.n_local):
+                raise ValueError(f"bool {'exclusions' if rows else 'mask'} must be {ndim}-d over the "
+                                 f"{self.n} global or {self.n_local} local items, got {tuple(g.shape)}")
+            loc = g[..., self.lo:self.hi] if g.shape[-1] == self.n else g
+            return torch.as_tensor(bits_from_bool(loc).view(np.int32)).to(self._device())
+        t = a if is_t else torch.from_numpy(np.ascontiguousarray(a))
+        if t.dtype not in (torch.int32, torch.uint32) or t.dim() != ndim or t.shape[-1] != self.words:
+            raise ValueError(f"packed {'exclusions' if rows else 'mask'} must be int32/uint32 words of this "
+                             f"rank's rows, shape {'(B, ' if rows else '('}{self.words}), got {tuple(t.shape)} "
+                             f"{t.dtype}")
+        if t.dtype == torch.uint32:
+            t = t.view(torch.int32)
+        return t.to(self._device()).contiguous()
 
     # ---------------------------------------------------------------- search
     def query_rows(self, item_ids):

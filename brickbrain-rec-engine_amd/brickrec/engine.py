@@ -85,7 +85,9 @@ class ItemIndex:
         h = C.c_void_p()
         L.check(self._lib.bb_create(C.byref(desc), C.byref(h)), "bb_create")
         self._h = h
-        self._mu = threading.Lock()
+        # re-entrant: close() can run from __del__ (cyclic GC) on a thread already holding this
+        # lock inside view() / search(), and takes the view's and then the base's lock
+        self._mu = threading.RLock()
         self.n_items = 0
         self.d = 0
         self.r = 0
@@ -102,7 +104,7 @@ class ItemIndex:
             L.check(self._lib.bb_create_view(self._h, C.byref(h)), "bb_create_view")
             self._views = getattr(self, "_views", 0) + 1
         v._h = h
-        v._mu = threading.Lock()
+        v._mu = threading.RLock()
         v.n_items, v.d, v.r = self.n_items, self.d, self.r
         v._base = self  # keeps the base alive while the view is
         return v
@@ -456,10 +458,11 @@ class ItemIndex:
     def set_option(self, option: str, value: int):
         """Tuning knobs: "stream" (-1 auto / 0 off / 1 on), "stream_min_items", "workspace_bytes",
         "stream_refine" (-1 auto / 0 off / 1 on: the two-level streaming bound), "rr_lists" (-1 auto
-        / 0 off: bounded candidate lists instead of a score image on one-slab f32 searches)."""
+        / 0 off: bounded candidate lists instead of a score image on one-slab f32 searches),
+        "small_batch" (-1 auto / 0 off: the one-pass exact search of batches of <= 16 rows)."""
         code = {"stream": L.BB_OPT_STREAM, "stream_min_items": L.BB_OPT_STREAM_MIN_ITEMS,
                 "workspace_bytes": L.BB_OPT_WORKSPACE_BYTES, "stream_refine": L.BB_OPT_STREAM_REFINE,
-                "rr_lists": L.BB_OPT_RR_LISTS}[option]
+                "rr_lists": L.BB_OPT_RR_LISTS, "small_batch": L.BB_OPT_SMALL_BATCH}[option]
         with self._mu:
             L.check(self._lib.bb_set_option(self._h, code, int(value)), "bb_set_option")
 

@@ -87,6 +87,7 @@ struct bb_index {
   int64_t stream_min_items = 100000;   // BB_OPT_STREAM_MIN_ITEMS
   int refine_opt = -1;                 // BB_OPT_STREAM_REFINE
   int lists_opt = -1;                  // BB_OPT_RR_LISTS
+  int sq_opt = -1;                     // BB_OPT_SMALL_BATCH
   bb_index* base = nullptr;            // a view (bb_create_view): the handle owning the rows
   std::atomic<int> n_views{0};         // views of this handle still alive
   hipStream_t stream = nullptr;
@@ -123,6 +124,7 @@ struct bb_index {
   DevBuf rr_flags;     // one-wave re-rank select: rows left to the block select
   DevBuf list1, max1;  // two-level streaming: exact top-K_int (+ rank-0 key) of items [0, n1)
   DevBuf lists, r0lists;  // bounded candidate lists of the list scans (list_epi.h), both sides
+  DevBuf sq_top, sq_pmax, sq_ords, sq_ticket;  // small-batch exact search (sq.hip)
   uint32_t* ovf_host = nullptr;  // pinned
 
   bool prof = false;
@@ -304,6 +306,7 @@ int bb_create_view(bb_index* b, bb_index** out) {
   x->stream_min_items = b->stream_min_items;
   x->refine_opt = b->refine_opt;
   x->lists_opt = b->lists_opt;
+  x->sq_opt = b->sq_opt;
   x->n = b->n;
   x->Npad = b->Npad;
   x->d = b->d;
@@ -355,7 +358,8 @@ int bb_destroy(bb_index* x) {
                       &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
                       &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
                       &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
-                      &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists, &x->pilot_top})
+                      &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists, &x->pilot_top,
+                      &x->sq_top, &x->sq_pmax, &x->sq_ords, &x->sq_ticket})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
     if (x->has_last) (void)hipEventSynchronize(x->done);
@@ -722,6 +726,83 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       (rc = to_device(x, x->stage_in, off_mask, q->mask_bits, b_mask, where, s, &d_mask)) ||
       (rc = to_device(x, x->stage_in, off_excl, q->excl_bits, b_excl, where, s, &d_excl)))
     return rc;
+
+  // ---- small batches (the reference's request shape: one target row, one user, one
+  // retriever query): one exact pass over the f32 rows (sq.hip) instead of the approximate
+  // scan + lists + re-rank.  BB_OPT_SMALL_BATCH / BB_SQ (A/B runs): 0 off, 1 on with the merge
+  // as its own launch, 2 on with the merge in the last workgroup (one launch), -1 auto. ----
+  static const int sq_env = ab_env("BB_SQ") ? atoi(ab_env("BB_SQ")) : -1;
+  const int sq_sel = x->sq_opt >= 0 ? x->sq_opt : sq_env;
+  const int64_t sq_ld = need_cf ? x->Rpad : x->Dpad;
+  if (sq_sel != 0 && x->dtype == F32 && sides == 1 && B <= kSqMaxB && K_int <= kSqMaxK &&
+      sq_ld <= kRrMaxD && (need_cf ? x->r : x->d) <= kRrMaxD && x->n <= (int64_t)kSqMaxWg * kSqMaxRows) {
+    static const int sq_wg_env = ab_env("BB_SQ_WG") ? atoi(ab_env("BB_SQ_WG")) : 256;
+    const bool sq_fused = sq_sel == 2;
+    SqArgs a{};
+    a.X = (const float*)(need_cf ? x->cf.p : x->items.p);
+    a.ldx = sq_ld;
+    a.n = (int32_t)x->n;
+    a.gid0 = (uint32_t)x->id_offset;
+    a.present = (const uint32_t*)(need_cf ? x->cf_present.p : x->items_present.p);
+    a.mask = (const uint32_t*)d_mask;
+    a.excl = need_cf ? (const uint32_t*)d_excl : nullptr;  // rated items: the CF side only (as the scans)
+    a.excl_ld = nw;
+    a.drop = drop;
+    a.B = B;
+    if (q->mode == BB_MODE_SEMANTIC || (q->mode == BB_MODE_SIMILAR && !d_items) || need_cf) {
+      a.q_kind = q->mode == BB_MODE_SEMANTIC ? 0 : 2;
+      a.q_src = need_cf ? d_cf : d_rows;
+      a.q_dtype = need_cf ? q->q_cf_dtype : q->q_dtype;
+      a.q_ld = a.q_d = need_cf ? x->r : x->d;
+    } else {
+      a.q_kind = 1;
+      a.q_ids = (const int64_t*)d_items;
+      a.q_id_offset = x->id_offset;
+    }
+    const int64_t wg_goal = std::max(1, std::min(sq_wg_env, kSqMaxWg));
+    a.rpw = (int32_t)std::min<int64_t>(kSqMaxRows, std::max<int64_t>(4, round_up((x->n + wg_goal - 1) / wg_goal, 4)));
+    a.nwg = (int32_t)((x->n + a.rpw - 1) / a.rpw);
+    a.K = K_int;
+    if ((rc = x->sq_top.ensure((size_t)B * a.nwg * kSqM * 8)) || (rc = x->sq_pmax.ensure((size_t)B * a.nwg * 8)) ||
+        (rc = x->sq_ords.ensure((size_t)B * x->n * 4)) || (rc = x->keys.ensure((size_t)B * K_int * 8)) ||
+        (rc = x->maxk.ensure((size_t)B * 8)))
+      return rc;
+    if (!x->sq_ticket.p) {
+      if ((rc = x->sq_ticket.ensure(64))) return rc;
+      BB_HIP(hipMemsetAsync(x->sq_ticket.p, 0, 64, s));
+    }
+    a.wg_top = (uint64_t*)x->sq_top.p;
+    a.wg_pmax = (uint64_t*)x->sq_pmax.p;
+    a.ords = (uint32_t*)x->sq_ords.p;
+    a.ords_ld = x->n;
+    a.ticket = sq_fused ? (unsigned long long*)x->sq_ticket.p : nullptr;
+    const bool host_res = !out_keys && res->where != BB_DEVICE;
+    if (host_res && ((rc = x->out_sc.ensure((size_t)B * q->k * 4)) || (rc = x->out_id.ensure((size_t)B * q->k * 8)) ||
+                     (rc = x->out_cnt.ensure((size_t)B * 4))))
+      return rc;
+    if (out_keys) {
+      a.keys_out = (uint64_t*)x->keys.p;
+      a.max_out = (uint64_t*)x->maxk.p;
+    } else {
+      a.k_final = q->k;
+      a.out_scores = host_res ? (float*)x->out_sc.p : res->scores;
+      a.out_ids = host_res ? (int64_t*)x->out_id.p : res->ids;
+      a.out_counts = host_res ? (int32_t*)x->out_cnt.p : res->counts;
+    }
+    if ((rc = timed(x, K_GEMM, s, [&] { return launch_sq_scan(a, s); }))) return rc;
+    if (!a.ticket && (rc = timed(x, K_SELECT, s, [&] { return launch_sq_merge(a, s); }))) return rc;
+    if (out_keys) {
+      const hipMemcpyKind kind = res->where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+      BB_HIP(hipMemcpyAsync(res->keys, a.keys_out, (size_t)B * K_int * 8, kind, s));
+      BB_HIP(hipMemcpyAsync(res->max_keys, a.max_out, (size_t)B * 8, kind, s));
+    } else if (host_res) {
+      BB_HIP(hipMemcpyAsync(res->scores, a.out_scores, (size_t)B * q->k * 4, hipMemcpyDeviceToHost, s));
+      BB_HIP(hipMemcpyAsync(res->ids, a.out_ids, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
+      if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, a.out_counts, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+    }
+    if (host_res || where == BB_HOST || (out_keys && res->where != BB_DEVICE)) BB_HIP(hipStreamSynchronize(s));
+    return BB_OK;
+  }
 
   // workspace
   const size_t es = elem_size(x->dtype);
@@ -1552,6 +1633,10 @@ int bb_set_option(bb_index* x, int32_t option, int64_t value) {
     case BB_OPT_RR_LISTS:
       if (value < -1 || value > 1) return fail(BB_E_ARG, "BB_OPT_RR_LISTS must be -1, 0 or 1");
       x->lists_opt = (int)value;
+      return BB_OK;
+    case BB_OPT_SMALL_BATCH:
+      if (value < -1 || value > 2) return fail(BB_E_ARG, "BB_OPT_SMALL_BATCH must be -1, 0, 1 or 2");
+      x->sq_opt = (int)value;
       return BB_OK;
     case BB_OPT_WORKSPACE_BYTES:
       if (value < (1ll << 20)) return fail(BB_E_ARG, "BB_OPT_WORKSPACE_BYTES must be >= 1 MiB");

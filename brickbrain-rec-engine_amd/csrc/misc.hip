@@ -163,35 +163,6 @@ hipError_t launch_rr_prepare(const float* src, int64_t npad, int64_t ld_f, uint1
 // normalised) item rows of the liked sets (similar-sets: the query IS feat_matrix[target],
 // recommendation_system.py:213), or copy user factor rows (CF, :435).  Rows >= B are zero.
 // ---------------------------------------------------------------------------------------
-// Load C elements per lane (i = base + lane + 64c, zero past `d`) with the dtype switch
-// outside the loads, so all C loads are in flight together.
-template <int C>
-__device__ __forceinline__ void load_chunk(const void* p, int dt, size_t sb, int base, int d, int lane,
-                                           double (&x)[C]) {
-  if (dt == F32) {
-    const float* q = (const float*)p + sb;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int i = base + lane + 64 * c;
-      x[c] = i < d ? (double)q[i] : 0.0;
-    }
-  } else if (dt == F64) {
-    const double* q = (const double*)p + sb;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int i = base + lane + 64 * c;
-      x[c] = i < d ? q[i] : 0.0;
-    }
-  } else {
-    const uint16_t* q = (const uint16_t*)p + sb;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int i = base + lane + 64 * c;
-      x[c] = i < d ? (double)__builtin_bit_cast(float, (uint32_t)q[i] << 16) : 0.0;
-    }
-  }
-}
-
 constexpr int kPrepC = kQnC;  // rows up to 512 wide stay in registers (one load round)
 
 // f32 -> three bf16 planes (x = xh + xm + xl exactly) for the split-precision scan

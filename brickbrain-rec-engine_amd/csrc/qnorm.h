@@ -32,4 +32,36 @@ __device__ __forceinline__ double qn_norm(const double (&x)[kQnC]) {
 
 __device__ __forceinline__ float qn_elem(double x, double nrm) { return (float)(x / nrm); }
 
+// Load C elements per lane (i = base + lane + 64c, zero past `d`) with the dtype switch
+// outside the loads, so all C loads are in flight together: every load is unconditional (the
+// index clamped to the row, d >= 1) and the zero is selected afterwards — a conditional load
+// puts each element in a basic block of its own behind its own s_waitcnt vmcnt(0).
+template <int C>
+__device__ __forceinline__ void load_chunk(const void* p, int dt, size_t sb, int base, int d, int lane,
+                                           double (&x)[C]) {
+  if (dt == F32) {
+    const float* q = (const float*)p + sb;
+    float v[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) v[c] = q[min(base + lane + 64 * c, d - 1)];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = base + lane + 64 * c < d ? (double)v[c] : 0.0;
+  } else if (dt == F64) {
+    const double* q = (const double*)p + sb;
+    double v[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) v[c] = q[min(base + lane + 64 * c, d - 1)];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = base + lane + 64 * c < d ? v[c] : 0.0;
+  } else {
+    const uint16_t* q = (const uint16_t*)p + sb;
+    uint32_t v[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) v[c] = q[min(base + lane + 64 * c, d - 1)];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      x[c] = base + lane + 64 * c < d ? (double)__builtin_bit_cast(float, v[c] << 16) : 0.0;
+  }
+}
+
 }  // namespace bb

@@ -681,19 +681,21 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     // ties the accumulator to a wait long enough for the last MFMA to retire, before any
     // register copy or read of it the compiler may place after this point.
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" : "+v"(c));
+    // The eligibility words were loaded by asm (destinations count as written at the asm's
+    // end): the wait names them "+v" in the SAME statement, so no use or copy of them moves
+    // before it; between the loads and this wait nothing may touch those registers, which
+    // tests/test_asm_hazard.py checks on the shipped code object (CFG walk, vmcnt counted).
     if constexpr (!(ABL & 4)) {
       // the last PIECES vector-memory ops are tile + 2's DMA (the staging slices come
       // last, asm "memory" clobbers keep that order): leave them in flight
       if constexpr (ABL & 2)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(nw_p), "+v"(nw_m), "+v"(nw_e) : : "memory");
       else
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(nw_p), "+v"(nw_m), "+v"(nw_e) : "n"(PIECES) : "memory");
       __syncthreads();
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (probe) the asm word loads
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(nw_p), "+v"(nw_m), "+v"(nw_e) : : "memory");  // (probe)
     }
-    // the words are complete here; the tie keeps every use of them after the wait
-    asm volatile("" : "+v"(nw_p), "+v"(nw_m), "+v"(nw_e));
     pw = nw_p;
     mw = nw_m;
     ew = nw_e;

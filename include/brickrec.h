@@ -200,12 +200,19 @@ int bb_get_profile(bb_index* idx, bb_profile* out);
  *   BB_OPT_RR_LISTS         -1 auto (default, = 1), 0 off: one-slab searches of an f32 index
  *                           keep bounded per-lane candidate lists in the scan instead of
  *                           writing a score image for the select (no B×n image).  Results are
- *                           identical either way. */
+ *                           identical either way.
+ *   BB_OPT_SMALL_BATCH      -1 auto (default), 0 off, 1 on (merge as its own launch), 2 on
+ *                           (merge in the last workgroup: one launch): batches of up to 16
+ *                           query rows of one side (semantic / similar / CF) on an f32 index
+ *                           of up to 131,072 rows take one exact pass over the f32 rows (every
+ *                           score exact, no approximate scan or re-rank) — the reference's
+ *                           one-query request shape.  Results are identical either way. */
 #define BB_OPT_STREAM 1
 #define BB_OPT_STREAM_MIN_ITEMS 2
 #define BB_OPT_WORKSPACE_BYTES 3
 #define BB_OPT_STREAM_REFINE 4
 #define BB_OPT_RR_LISTS 5
+#define BB_OPT_SMALL_BATCH 6
 int bb_set_option(bb_index* idx, int32_t option, int64_t value);
 
 /* Stored (normalised, index-dtype) item rows of B global ids into out (B×d, row-major;

@@ -1,0 +1,53 @@
+"""The inline-asm eligibility loads of scan2_kernel.h: on the SHIPPED
+library, no instruction names a `global_load_dword` destination register between the load and
+a `s_waitcnt vmcnt` that retires it, on any control-flow path (tools/vmem_hazard_check.py).
+CPU only: the code object is extracted and disassembled with the ROCm LLVM tools."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import vmem_hazard_check as H  # noqa: E402
+
+needs_tools = pytest.mark.skipif(not os.path.exists(os.path.join(H.LLVM, "llvm-objdump")),
+                                 reason="ROCm LLVM tools absent")
+
+
+def _fn(lines):
+    return [(0x100 + 4 * i, mn, ops) for i, (mn, ops) in enumerate(lines)]
+
+
+def test_checker_flags_a_read_before_the_wait():
+    insns = _fn([("global_load_dword", "v7, v[2:3], off"), ("global_load_lds_dwordx4", "v[4:5], off"),
+                 ("v_mov_b32_e32", "v9, v7"), ("s_waitcnt", "vmcnt(1)"), ("v_add_u32_e32", "v1, v7, v1")])
+    n, bad = H.check_function("k", insns)
+    assert n == 1 and len(bad) == 1 and "v_mov_b32_e32" in bad[0]
+
+
+def test_checker_counts_vmcnt_and_follows_branches():
+    ok = _fn([("global_load_dword", "v7, v[2:3], off"), ("global_load_lds_dwordx4", "v[4:5], off"),
+              ("s_waitcnt", "vmcnt(1)"), ("v_add_u32_e32", "v1, v7, v1"), ("s_endpgm", "")])
+    assert H.check_function("k", ok) == (1, [])
+    # vmcnt(2) with only one later op leaves the load in flight: the use is a violation
+    early = _fn([("global_load_dword", "v7, v[2:3], off"), ("global_load_lds_dwordx4", "v[4:5], off"),
+                 ("s_waitcnt", "vmcnt(2)"), ("v_add_u32_e32", "v1, v7, v1"), ("s_endpgm", "")])
+    assert len(H.check_function("k", early)[1]) == 1
+    # the taken side of a branch reads the register: caught
+    br = [(0x100, "global_load_dword", "v7, v[2:3], off"),
+          (0x104, "s_cbranch_scc1", "2 // <k+0x10>"),
+          (0x108, "s_waitcnt", "vmcnt(0)"),
+          (0x10c, "s_endpgm", ""),
+          (0x110, "v_mov_b32_e32", "v8, v7"),
+          (0x114, "s_endpgm", "")]
+    assert len(H.check_function("k", br)[1]) == 1
+
+
+@needs_tools
+def test_shipped_scan2_loads_are_retired_before_use():
+    kernels, sites, bad = H.run()
+    assert kernels >= 8, kernels          # every scan2 instantiation of the build
+    assert sites >= 100, sites            # not a vacuous pass
+    assert not bad, "\n".join(bad[:10])

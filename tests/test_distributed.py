@@ -196,3 +196,49 @@ def test_empty_shard_world4():
         for mode in outs[0]:
             for a, b_ in zip(outs[0][mode], outs[r][mode]):
                 np.testing.assert_array_equal(a, b_)
+
+
+def _single_rank_index(n):
+    """A ShardedIndex of one gloo rank over OracleShard (its own process group)."""
+    import socket
+    import torch.distributed as dist
+    from _oracle_shard import OracleShard
+    from brickrec.distributed import ShardedIndex
+    if not dist.is_initialized():
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    return ShardedIndex(n, index_factory=OracleShard)
+
+
+def test_local_bits_rejects_foreign_packed_words():
+    """packed words must be this rank's — a bitset of the wrong length (global,
+    another rank's, or a uint32 word array of another size) raises instead of reaching the
+    kernel; bool arrays are packed; int32 / uint32 words of the right shape pass through."""
+    import torch
+    si = _single_rank_index(100)
+    W = si.words
+    good = torch.zeros(W, dtype=torch.int32)
+    assert si._local_bits(good, False).shape == (W,)
+    assert si._local_bits(np.zeros(W, np.uint32), False).dtype == torch.int32
+    assert si._local_bits(np.zeros((3, W), np.uint32), True).shape == (3, W)
+    assert si._local_bits(np.ones(100, bool), False).shape == (W,)
+    for bad, rows in ((torch.zeros(W + 1, dtype=torch.int32), False), (np.zeros(W * 2, np.uint32), False),
+                      (torch.zeros((2, W), dtype=torch.int32), False), (np.zeros(W, np.int32), True),
+                      (torch.zeros(W, dtype=torch.int64), False), (np.ones(77, bool), False)):
+        with pytest.raises(ValueError):
+            si._local_bits(bad, rows)
+
+
+def test_excl_bits_tensor_repeats_count_once():
+    """a repeated id in a padded [B, m] tensor sets its bit once (the scatter adds,
+    so a duplicate would carry into the next bit)."""
+    import torch
+    si = _single_rank_index(100)
+    ids = torch.tensor([[5, 5, 7, -1], [31, 31, 31, 0]])
+    w = si.excl_bits(ids).numpy().view(np.uint32)
+    assert w[0, 0] == (1 << 5) | (1 << 7)
+    assert w[1, 0] == (1 << 31) | 1
+    ref = si.excl_bits([[5, 7], [0, 31]]).numpy()
+    assert np.array_equal(w.view(np.int32), ref)

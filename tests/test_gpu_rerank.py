@@ -219,7 +219,9 @@ np.savez(sys.argv[3], sc=sc, ids=ids, s2=s2, i2=i2)
 def test_rr_lists_vs_image_identical(brickrec):
     """The bounded candidate lists (BB_OPT_RR_LISTS, default on: no score image) and the int16
     score image + select path give the same bits: semantic, similar-sets with a mask (rank 0
-    masked or not), CF with rated exclusions and the hybrid blend, at B = 1, 37 and 256."""
+    masked or not), CF with rated exclusions and the hybrid blend, at B = 1, 37, 256 and 1024
+    (scan4's list epilogue, the dual list scan and the dual list select).  The small-batch
+    path (which takes B = 1 otherwise) is off here: the lists themselves are under test."""
     rng = np.random.default_rng(21)
     n, d, r, k = 25216, 384, 50, 50
     x = R.unit_rows(n, d, 5)
@@ -229,7 +231,8 @@ def test_rr_lists_vs_image_identical(brickrec):
     idx = brickrec.ItemIndex(dtype="f32")
     idx.upload_items(x)
     idx.upload_cf(f)
-    for B in (1, 37, 256):
+    idx.set_option("small_batch", 0)
+    for B in (1, 37, 256, 1024):
         q = rng.standard_normal((B, d)).astype(np.float32)
         qi = rng.choice(n, B, replace=False)
         qi[0] = 7000

@@ -1,0 +1,271 @@
+"""GPU parity of the small-batch exact search (csrc/sq.hip): batches of <= 16 query rows of one
+side on an f32 index take ONE pass over the f32 rows with every score exact (f32 products
+summed in f64 in rescore_rows' fixed order, rounded to f32) — the reference's own request
+shape: one target row (get_similar_sets, recommendation_system.py:213-217), one user row (CF,
+:438-461), one retriever query with k = 20 (lego_nlp_recommeder.py:305, 1394).
+
+Every case runs three ways on the same index and inputs — the large-batch path (bf16 MFMA scan
++ candidate lists + exact re-rank, BB_OPT_SMALL_BATCH = 0), the small-batch path with its merge
+as a second launch (1), and with the merge in the last workgroup (2, one launch) — and the
+lists must be identical bit for bit (ids and score bits); they are also checked against an f64
+recompute over the device's own f32 operands.  Edge cases: ragged batches (every B in 1..16),
+k > eligible items, an empty mask, a workgroup holding many of the top items (its list
+overflows), masses of equal scores (more than 256 candidates: the exact fallback), rank 0
+duplicated, the BB_Q_OUT_KEYS lists of a sharded search, and a tiny index (G5's 10 rows).
+"""
+import numpy as np
+import pytest
+
+from oracle import restatement as R
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = (0, 1, 2)
+
+
+@pytest.fixture(scope="module")
+def brickrec():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+    import brickrec as br
+    return br
+
+
+def _qop(q):
+    q64 = q.astype(np.float64)
+    n = np.sqrt((q64 * q64).sum(1, keepdims=True))
+    n[n == 0] = 1.0
+    return (q64 / n).astype(np.float32)
+
+
+def _exact(rows32, q32, k, allowed, drop_present=None):
+    s = (rows32.astype(np.float64) @ q32.astype(np.float64)).astype(np.float32)
+    ok = allowed.copy()
+    if drop_present is not None:
+        p = np.where(drop_present, s, -np.inf)
+        r0 = int(np.flatnonzero(p == p.max())[0])
+        ok[r0] = False
+    idx = np.flatnonzero(ok)
+    o = np.lexsort((idx, -s[idx]))[:k]
+    return idx[o], s[idx[o]]
+
+
+def _run(idx, variant, *args, **kw):
+    idx.set_option("small_batch", variant)
+    try:
+        return idx.search(*args, **kw)
+    finally:
+        idx.set_option("small_batch", -1)
+
+
+def _same(a, b):
+    sa, ia, ca = a
+    sb, ib, cb = b
+    assert np.array_equal(ca, cb), (ca, cb)
+    assert np.array_equal(ia, ib)
+    assert np.array_equal(sa.view(np.uint32), sb.view(np.uint32))
+
+
+def _all_variants(idx, *args, **kw):
+    outs = [_run(idx, v, *args, **kw) for v in VARIANTS]
+    _same(outs[0], outs[1])
+    _same(outs[0], outs[2])
+    return outs[1]
+
+
+@pytest.fixture(scope="module")
+def c1(brickrec):
+    n, d = 25216, 384
+    x = R.unit_rows(n, d, 1234)
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(x, prenormalized=True)
+    rows = idx.get_rows(np.arange(n))
+    yield idx, x, rows
+    idx.close()
+
+
+@pytest.mark.parametrize("B", list(range(1, 17)))
+def test_semantic_every_batch_size(c1, B):
+    idx, x, rows = c1
+    k = 10 if B == 1 else 50
+    q = R.unit_rows(B, 384, 500 + B) * 3.0  # raw rows: the path normalises them
+    sc, ids, cnt = _all_variants(idx, "semantic", k, q_rows=q)
+    qn = _qop(q)
+    allowed = np.ones(len(rows), bool)
+    for b in range(B):
+        ri, rs = _exact(rows, qn[b], k, allowed)
+        assert list(ids[b]) == list(ri)
+        assert np.array_equal(sc[b].view(np.uint32), rs.view(np.uint32))
+        assert cnt[b] == k
+
+
+def test_retriever_k20_and_k128(c1):
+    idx, x, rows = c1
+    q = R.unit_rows(3, 384, 77)
+    for k in (20, 127):  # K_int <= 128: the small-batch bound
+        _all_variants(idx, "semantic", k, q_rows=q)
+
+
+def test_similar_with_mask_rank0_dropped(c1):
+    idx, x, rows = c1
+    rng = np.random.default_rng(3)
+    liked = rng.choice(len(rows), 12, replace=False)
+    mask = rng.random(len(rows)) < 0.1
+    mask[liked[:6]] = True    # rank 0 (the liked row itself) inside and outside the mask
+    mask[liked[6:]] = False
+    sc, ids, cnt = _all_variants(idx, "similar", 10, q_items=liked, mask=mask)
+    for b, t in enumerate(liked):
+        ri, rs = _exact(rows, rows[t], 10, mask, drop_present=np.ones(len(rows), bool))
+        assert list(ids[b]) == list(ri)
+        assert np.array_equal(sc[b].view(np.uint32), rs.view(np.uint32))
+
+
+def test_similar_duplicate_rank0(brickrec):
+    """A duplicate of the target outranks nothing: ties at rank 0 drop the lower id (the
+    arg-max of the (score desc, id asc) order), and the target itself may survive."""
+    n, d = 5000, 64
+    x = R.unit_rows(n, d, 9)
+    x[4321] = x[17]
+    x[2000] = x[17]
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x, prenormalized=True)
+        rows = idx.get_rows(np.arange(n))
+        sc, ids, cnt = _all_variants(idx, "similar", 5, q_items=np.array([4321, 17, 99]))
+        for b, t in enumerate((4321, 17, 99)):
+            ri, rs = _exact(rows, rows[t], 5, np.ones(n, bool), drop_present=np.ones(n, bool))
+            assert list(ids[b]) == list(ri)
+    finally:
+        idx.close()
+
+
+def test_cf_rated_excluded(brickrec):
+    n, r, B = 25216, 50, 7
+    rng = np.random.default_rng(11)
+    x = R.unit_rows(n, 384, 5)
+    f = rng.normal(0, 0.1, (n, r)).astype(np.float32)
+    present = rng.random(n) < 0.9
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x, prenormalized=True)
+        idx.upload_cf(f, present=present)
+        u = rng.normal(0, 0.1, (B, r)).astype(np.float32)
+        rated = np.zeros((B, n), bool)
+        for b in range(B):
+            rated[b, rng.choice(n, 30, replace=False)] = True
+        mask = rng.random(n) < 0.5
+        sc, ids, cnt = _all_variants(idx, "cf", 20, q_cf=u, mask=mask, excl=rated)
+        f32 = f.astype(np.float32)
+        for b in range(B):
+            ri, rs = _exact(f32, u[b], 20, mask & present & ~rated[b])
+            assert list(ids[b]) == list(ri)
+            assert np.array_equal(sc[b].view(np.uint32), rs.view(np.uint32))
+    finally:
+        idx.close()
+
+
+def test_k_beyond_eligible_and_empty_mask(c1):
+    idx, x, rows = c1
+    q = R.unit_rows(2, 384, 8)
+    mask = np.zeros(len(rows), bool)
+    mask[[5, 900, 25000]] = True
+    sc, ids, cnt = _all_variants(idx, "semantic", 10, q_rows=q, mask=mask)
+    assert list(cnt) == [3, 3]
+    assert (ids[:, 3:] == -1).all() and (sc[:, 3:] == 0).all()
+    sc, ids, cnt = _all_variants(idx, "semantic", 10, q_rows=q, mask=np.zeros(len(rows), bool))
+    assert list(cnt) == [0, 0] and (ids == -1).all()
+
+
+def test_overflowed_workgroup_list(brickrec):
+    """One workgroup's rows hold the whole top-20 (consecutive near-copies of the query): its
+    list of 4 overflows and the merge takes that workgroup's rows from their order images."""
+    n, d = 20000, 128
+    x = R.unit_rows(n, d, 21)
+    q = R.unit_rows(1, d, 22)[0]
+    rng = np.random.default_rng(1)
+    for i in range(40):
+        v = q + 0.02 * rng.standard_normal(d)
+        x[3000 + i] = v / np.linalg.norm(v)
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x, prenormalized=True)
+        rows = idx.get_rows(np.arange(n))
+        sc, ids, cnt = _all_variants(idx, "semantic", 30, q_rows=q[None, :])
+        ri, rs = _exact(rows, _qop(q[None, :])[0], 30, np.ones(n, bool))
+        assert list(ids[0]) == list(ri)
+        assert 3000 <= ids[0][0] < 3040
+    finally:
+        idx.close()
+
+
+def test_masses_of_equal_scores_fallback(brickrec):
+    """600 identical rows tie at the top: more than 256 candidates reach the bound, so the merge
+    runs the exact wave fallback; ties resolve by id ascending."""
+    n, d = 30000, 96
+    x = R.unit_rows(n, d, 31)
+    q = R.unit_rows(1, d, 32)[0]
+    dup = np.sort(np.random.default_rng(2).choice(n, 600, replace=False))
+    x[dup] = q
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x, prenormalized=True)
+        sc, ids, cnt = _all_variants(idx, "semantic", 100, q_rows=q[None, :])
+        assert list(ids[0]) == list(dup[:100])
+        assert len(set(sc[0].view(np.uint32))) == 1
+    finally:
+        idx.close()
+
+
+def test_out_keys_sharded_lists(c1, brickrec):
+    import torch
+    idx, x, rows = c1
+    q = torch.from_numpy(R.unit_rows(5, 384, 41)).cuda()
+    liked = torch.tensor([3, 77, 25000], device="cuda")
+    outs = {}
+    for v in VARIANTS:
+        idx.set_option("small_batch", v)
+        try:
+            outs[v] = (idx.search_keys("semantic", 50, q_rows=q), idx.search_keys("similar", 10, q_items=liked))
+        finally:
+            idx.set_option("small_batch", -1)
+    torch.cuda.synchronize()
+    for v in (1, 2):
+        for a, b in zip(outs[0], outs[v]):
+            assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+def test_tiny_index_g5(brickrec):
+    n, d = 10, 384
+    x = R.unit_rows(n, d, 51)
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x, prenormalized=True)
+        sc, ids, cnt = _all_variants(idx, "similar", 3, q_items=np.array([4, 1]))
+        rows = idx.get_rows(np.arange(n))
+        for b, t in enumerate((4, 1)):
+            ri, rs = _exact(rows, rows[t], 3, np.ones(n, bool), drop_present=np.ones(n, bool))
+            assert list(ids[b]) == list(ri)
+        sc, ids, cnt = _all_variants(idx, "semantic", 20, q_rows=x[:2])
+        assert list(cnt) == [10, 10]
+    finally:
+        idx.close()
+
+
+def test_device_inputs_and_views(c1, brickrec):
+    """Torch device tensors on a view's own stream (the bench's in-flight lanes)."""
+    import torch
+    idx, x, rows = c1
+    v = idx.view()
+    try:
+        q = torch.from_numpy(R.unit_rows(16, 384, 61)).cuda()
+        s = torch.cuda.Stream()
+        run, out = v.prepared_search("semantic", 50, q_rows=q, stream=s)
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        ref = idx.search("semantic", 50, q_rows=q.cpu().numpy())
+        assert np.array_equal(out[1].cpu().numpy(), ref[1])
+        assert np.array_equal(out[0].cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
+    finally:
+        v.close()
