@@ -459,6 +459,54 @@ def gpu_batch_sweep(brickrec, base, local, dev, seconds=0.5):
     return res
 
 
+def request_latency(brickrec, x, dev, reps=100):
+    """Serial p50 of single requests in the reference's own shapes (one call at a time on an
+    idle stream, HIP events): get_similar_sets top-10 (recommendation_system.py:194-249), the
+    pgvector retriever k=20 (lego_nlp_recommeder.py:305, 1394), CF top-20 of one user with
+    rated items excluded (:411-483), and HybridRecommender.get_recommendations top-10 with
+    the configs[2] mask and rated exclusions (:612-677) — f32 index with r=50 CF factors."""
+    import torch
+    rng = np.random.default_rng(77)
+    f = rng.normal(0.0, 0.1, (N_ITEMS, 50)).astype(np.float32)
+    idx = brickrec.ItemIndex(device=dev.index, dtype="f32")
+    idx.upload_items(x)
+    idx.upload_cf(f)
+    parts = rng.integers(1, 6000, N_ITEMS).astype(np.int32)
+    year = rng.integers(1949, 2025, N_ITEMS).astype(np.int16)
+    idx.upload_attrs(parts, year, rng.integers(0, 400, N_ITEMS).astype(np.int32))
+    mask = torch.from_numpy(brickrec.bits_from_bool(idx.eval_mask(brickrec.Predicate(parts_max=800, year_min=2015)))
+                            .view(np.int32)).to(dev)
+    rated = np.zeros((1, N_ITEMS), bool)
+    rated[0, rng.choice(N_ITEMS, 20, replace=False)] = True
+    excl = torch.from_numpy(brickrec.bits_from_bool(rated).view(np.int32)).to(dev)
+    liked = torch.tensor([int(rng.integers(N_ITEMS))], device=dev)
+    u = torch.from_numpy(rng.normal(0.0, 0.1, (1, 50)).astype(np.float32)).to(dev)
+    q = unit_rows_torch(1, DIM, 991, dev)
+    s = torch.cuda.Stream(dev)
+    cases = {"similar_k10": dict(mode="similar", k=10, q_items=liked),
+             "retriever_k20": dict(mode="semantic", k=20, q_rows=q),
+             "cf_k20_rated": dict(mode="cf", k=20, q_cf=u, excl=excl),
+             "hybrid_k10_mask_rated": dict(mode="hybrid", k=10, q_items=liked, q_cf=u, mask=mask, excl=excl)}
+    out = {}
+    for name, c in cases.items():
+        c = dict(c)
+        run, _ = idx.prepared_search(c.pop("mode"), c.pop("k"), stream=s, **c)
+        for _ in range(10):
+            run()
+        torch.cuda.synchronize()
+        ev = []
+        for _ in range(reps):
+            a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            run()
+            e.record(s)
+            ev.append((a, e))
+        torch.cuda.synchronize()
+        out[name] = round(float(np.median([a.elapsed_time(e) for a, e in ev])), 4)
+    idx.close()
+    return {"p50_ms_serial": out, "note": "B=1 requests on an idle stream, 25,216 x 384 f32 + r=50 CF"}
+
+
 def launch_ranks(args):
     """`--gpus N` without a launcher: start the N rank processes (torch.distributed.run on
     127.0.0.1, one rank per GPU) as a child before this process touches any GPU, and return
@@ -680,6 +728,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_sweep and not hybrid:
         out["gpu_batch_sweep"] = gpu_batch_sweep(brickrec, base, local, dev)
+        out["request_latency"] = request_latency(brickrec, x, dev)
     # rank 0 times the CPU baseline on every line (replicas: the same per-rank workload)
     if rank == 0 and not args.no_cpu and hybrid:
         x_np = x.cpu().numpy()

@@ -17,6 +17,7 @@
 #include "../../include/brickrec.h"
 #include "common.h"
 #include "list_epi.h"
+#include "sq.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -124,7 +125,7 @@ struct bb_index {
   DevBuf rr_flags;     // one-wave re-rank select: rows left to the block select
   DevBuf list1, max1;  // two-level streaming: exact top-K_int (+ rank-0 key) of items [0, n1)
   DevBuf lists, r0lists;  // bounded candidate lists of the list scans (list_epi.h), both sides
-  DevBuf sq_top, sq_pmax, sq_ords, sq_ticket;  // small-batch exact search (sq.hip)
+  DevBuf sq_top, sq_ptop, sq_ords, sq_q;  // small-batch exact search (sq.hip)
   uint32_t* ovf_host = nullptr;  // pinned
 
   bool prof = false;
@@ -359,7 +360,7 @@ int bb_destroy(bb_index* x) {
                       &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
                       &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
                       &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists, &x->pilot_top,
-                      &x->sq_top, &x->sq_pmax, &x->sq_ords, &x->sq_ticket})
+                      &x->sq_top, &x->sq_ptop, &x->sq_ords, &x->sq_q})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
     if (x->has_last) (void)hipEventSynchronize(x->done);
@@ -728,77 +729,117 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     return rc;
 
   // ---- small batches (the reference's request shape: one target row, one user, one
-  // retriever query): one exact pass over the f32 rows (sq.hip) instead of the approximate
-  // scan + lists + re-rank.  BB_OPT_SMALL_BATCH / BB_SQ (A/B runs): 0 off, 1 on with the merge
-  // as its own launch, 2 on with the merge in the last workgroup (one launch), -1 auto. ----
+  // retriever query, one HybridRecommender request): one approximate pass over the bf16 copy
+  // per side and an exact rescore of the candidates within its bound (sq.hip) instead of the
+  // MFMA scan + lists + list select; a hybrid search then blends the two sides' key lists in
+  // finalize1 as the large-batch path does.  BB_OPT_SMALL_BATCH / BB_SQ (A/B runs): 0 off,
+  // 1 on, -1 auto (on). ----
   static const int sq_env = ab_env("BB_SQ") ? atoi(ab_env("BB_SQ")) : -1;
   const int sq_sel = x->sq_opt >= 0 ? x->sq_opt : sq_env;
-  const int64_t sq_ld = need_cf ? x->Rpad : x->Dpad;
-  if (sq_sel != 0 && x->dtype == F32 && sides == 1 && B <= kSqMaxB && K_int <= kSqMaxK &&
-      sq_ld <= kRrMaxD && (need_cf ? x->r : x->d) <= kRrMaxD && x->n <= (int64_t)kSqMaxWg * kSqMaxRows) {
+  const bool sq_sides = (!need_content || (x->items_bf.p && x->Dpad <= kRrMaxD && x->d <= kRrMaxD && x->Dpad_b <= 512)) &&
+                        (!need_cf || (x->cf_bf.p && x->Rpad <= kRrMaxD && x->r <= kRrMaxD && x->Rpad_b <= 512));
+  if (sq_sel != 0 && x->dtype == F32 && B <= kSqMaxB && K_int <= kSqMaxK && sq_sides &&
+      x->n <= (int64_t)kSqMaxWg * kSqMaxRows) {
     static const int sq_wg_env = ab_env("BB_SQ_WG") ? atoi(ab_env("BB_SQ_WG")) : 256;
-    const bool sq_fused = sq_sel == 2;
-    SqArgs a{};
-    a.X = (const float*)(need_cf ? x->cf.p : x->items.p);
-    a.ldx = sq_ld;
-    a.n = (int32_t)x->n;
-    a.gid0 = (uint32_t)x->id_offset;
-    a.present = (const uint32_t*)(need_cf ? x->cf_present.p : x->items_present.p);
-    a.mask = (const uint32_t*)d_mask;
-    a.excl = need_cf ? (const uint32_t*)d_excl : nullptr;  // rated items: the CF side only (as the scans)
-    a.excl_ld = nw;
-    a.drop = drop;
-    a.B = B;
-    if (q->mode == BB_MODE_SEMANTIC || (q->mode == BB_MODE_SIMILAR && !d_items) || need_cf) {
-      a.q_kind = q->mode == BB_MODE_SEMANTIC ? 0 : 2;
-      a.q_src = need_cf ? d_cf : d_rows;
-      a.q_dtype = need_cf ? q->q_cf_dtype : q->q_dtype;
-      a.q_ld = a.q_d = need_cf ? x->r : x->d;
-    } else {
-      a.q_kind = 1;
-      a.q_ids = (const int64_t*)d_items;
-      a.q_id_offset = x->id_offset;
-    }
+    const bool hyb = sides == 2;
     const int64_t wg_goal = std::max(1, std::min(sq_wg_env, kSqMaxWg));
-    a.rpw = (int32_t)std::min<int64_t>(kSqMaxRows, std::max<int64_t>(4, round_up((x->n + wg_goal - 1) / wg_goal, 4)));
-    a.nwg = (int32_t)((x->n + a.rpw - 1) / a.rpw);
-    a.K = K_int;
-    if ((rc = x->sq_top.ensure((size_t)B * a.nwg * kSqM * 8)) || (rc = x->sq_pmax.ensure((size_t)B * a.nwg * 8)) ||
-        (rc = x->sq_ords.ensure((size_t)B * x->n * 4)) || (rc = x->keys.ensure((size_t)B * K_int * 8)) ||
-        (rc = x->maxk.ensure((size_t)B * 8)))
+    const int32_t rpw = (int32_t)std::min<int64_t>(kSqMaxRows, std::max<int64_t>(4, round_up((x->n + wg_goal - 1) / wg_goal, 4)));
+    const int32_t nwg = (int32_t)((x->n + rpw - 1) / rpw);
+    const size_t top_side = (size_t)B * nwg * kSqM, ord_side = (size_t)B * x->n * 2;
+    const size_t q_side = (size_t)B * kRrMaxD;
+    if ((rc = x->sq_top.ensure(top_side * 8 * sides)) || (rc = x->sq_ptop.ensure(top_side * 8)) ||
+        (rc = x->sq_ords.ensure(ord_side * 4 * sides)) || (rc = x->sq_q.ensure(q_side * 4 * sides)) ||
+        (rc = x->keys.ensure((size_t)sides * B * K_int * 8)) || (rc = x->maxk.ensure((size_t)B * 8)))
       return rc;
-    if (!x->sq_ticket.p) {
-      if ((rc = x->sq_ticket.ensure(64))) return rc;
-      BB_HIP(hipMemsetAsync(x->sq_ticket.p, 0, 64, s));
-    }
-    a.wg_top = (uint64_t*)x->sq_top.p;
-    a.wg_pmax = (uint64_t*)x->sq_pmax.p;
-    a.ords = (uint32_t*)x->sq_ords.p;
-    a.ords_ld = x->n;
-    a.ticket = sq_fused ? (unsigned long long*)x->sq_ticket.p : nullptr;
     const bool host_res = !out_keys && res->where != BB_DEVICE;
     if (host_res && ((rc = x->out_sc.ensure((size_t)B * q->k * 4)) || (rc = x->out_id.ensure((size_t)B * q->k * 8)) ||
                      (rc = x->out_cnt.ensure((size_t)B * 4))))
       return rc;
-    if (out_keys) {
-      a.keys_out = (uint64_t*)x->keys.p;
-      a.max_out = (uint64_t*)x->maxk.p;
-    } else {
-      a.k_final = q->k;
-      a.out_scores = host_res ? (float*)x->out_sc.p : res->scores;
-      a.out_ids = host_res ? (int64_t*)x->out_id.p : res->ids;
-      a.out_counts = host_res ? (int32_t*)x->out_cnt.p : res->counts;
-    }
-    if ((rc = timed(x, K_GEMM, s, [&] { return launch_sq_scan(a, s); }))) return rc;
-    if (!a.ticket && (rc = timed(x, K_SELECT, s, [&] { return launch_sq_merge(a, s); }))) return rc;
+    float* f_sc = host_res ? (float*)x->out_sc.p : res->scores;
+    int64_t* f_id = host_res ? (int64_t*)x->out_id.p : res->ids;
+    int32_t* f_cnt = host_res ? (int32_t*)x->out_cnt.p : res->counts;
+    // one side's pass: the content side (semantic / similar / hybrid side 0) or the CF side
+    auto side_args = [&](int side) {
+      const bool cf_side = q->mode == BB_MODE_CF || side == 1;
+      SqArgs a{};
+      a.Xb = (const uint16_t*)(cf_side ? x->cf_bf.p : x->items_bf.p);
+      a.ldb = cf_side ? x->Rpad_b : x->Dpad_b;
+      a.X = (const float*)(cf_side ? x->cf.p : x->items.p);
+      a.ldx = cf_side ? x->Rpad : x->Dpad;
+      a.stats = (const float*)x->rr_stats.p + (cf_side ? 4 : 0);
+      a.n = (int32_t)x->n;
+      a.gid0 = (uint32_t)x->id_offset;
+      a.present = (const uint32_t*)(cf_side ? x->cf_present.p : x->items_present.p);
+      a.mask = (const uint32_t*)d_mask;
+      a.excl = cf_side ? (const uint32_t*)d_excl : nullptr;  // rated items: the CF side only (as the scans)
+      a.excl_ld = nw;
+      a.drop = drop && side == 0;
+      a.B = B;
+      if (q->mode == BB_MODE_SEMANTIC || cf_side || !d_items) {
+        a.q_kind = q->mode == BB_MODE_SEMANTIC ? 0 : 2;
+        a.q_src = cf_side ? d_cf : d_rows;
+        a.q_dtype = cf_side ? q->q_cf_dtype : q->q_dtype;
+        a.q_ld = a.q_d = cf_side ? x->r : x->d;
+      } else {
+        a.q_kind = 1;
+        a.q_ids = (const int64_t*)d_items;
+        a.q_id_offset = x->id_offset;
+      }
+      a.q_out = (float*)x->sq_q.p + side * q_side;
+      a.rpw = rpw;
+      a.nwg = nwg;
+      a.K = K_int;
+      a.wg_top = (uint64_t*)x->sq_top.p + side * top_side;
+      a.wg_ptop = (uint64_t*)x->sq_ptop.p;  // (the rank-0 side only)
+      a.ords = (uint32_t*)x->sq_ords.p + side * ord_side;
+      a.ords_p = a.ords + (size_t)B * x->n;
+      a.ords_ld = x->n;
+      if (out_keys || hyb) {  // key lists (+ the present maximum) for a cross-shard merge or the blend
+        a.keys_out = (uint64_t*)x->keys.p + (size_t)side * B * K_int;
+        a.max_out = side == 0 ? (uint64_t*)x->maxk.p : nullptr;
+      } else {
+        a.k_final = q->k;
+        a.out_scores = f_sc;
+        a.out_ids = f_id;
+        a.out_counts = f_cnt;
+      }
+      return a;
+    };
+    const SqArgs a0 = side_args(0);
+    const SqArgs a1 = hyb ? side_args(1) : a0;
+    for (int side = 0; side < sides; ++side)
+      if ((rc = timed(x, K_GEMM, s, [&] { return launch_sq_scan(side ? a1 : a0, s); }))) return rc;
+    if ((rc = timed(x, K_SELECT, s, [&] { return launch_sq_merge(a0, hyb ? &a1 : nullptr, s); }))) return rc;
     if (out_keys) {
       const hipMemcpyKind kind = res->where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-      BB_HIP(hipMemcpyAsync(res->keys, a.keys_out, (size_t)B * K_int * 8, kind, s));
-      BB_HIP(hipMemcpyAsync(res->max_keys, a.max_out, (size_t)B * 8, kind, s));
-    } else if (host_res) {
-      BB_HIP(hipMemcpyAsync(res->scores, a.out_scores, (size_t)B * q->k * 4, hipMemcpyDeviceToHost, s));
-      BB_HIP(hipMemcpyAsync(res->ids, a.out_ids, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
-      if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, a.out_counts, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+      BB_HIP(hipMemcpyAsync(res->keys, x->keys.p, (size_t)sides * B * K_int * 8, kind, s));
+      if (drop) BB_HIP(hipMemcpyAsync(res->max_keys, x->maxk.p, (size_t)B * 8, kind, s));
+      else if (res->where == BB_DEVICE) BB_HIP(hipMemsetAsync(res->max_keys, 0, (size_t)B * 8, s));
+      else memset(res->max_keys, 0, (size_t)B * 8);
+    } else if (hyb) {  // the union blend of _combine_recommendations (:789-843), as the large-batch path
+      FinalizeArgs fa{};
+      fa.keys = (const uint64_t*)x->keys.p;
+      fa.max_keys = (const uint64_t*)x->maxk.p;
+      fa.P = 1;
+      fa.sides = 2;
+      fa.B = B;
+      fa.K_int = K_int;
+      fa.drop_rank0 = 1;
+      fa.k = q->k;
+      fa.k_side = q->k_side > 0 ? q->k_side : 2 * q->k;
+      fa.hybrid = 1;
+      fa.w_content = q->w_content;
+      fa.w_cf = q->w_cf;
+      fa.scores = f_sc;
+      fa.ids = f_id;
+      fa.counts = f_cnt;
+      fa.n_rows = B;
+      if ((rc = timed(x, K_FIN, s, [&] { return launch_finalize(fa, s); }))) return rc;
+    }
+    if (host_res) {
+      BB_HIP(hipMemcpyAsync(res->scores, f_sc, (size_t)B * q->k * 4, hipMemcpyDeviceToHost, s));
+      BB_HIP(hipMemcpyAsync(res->ids, f_id, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
+      if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, f_cnt, (size_t)B * 4, hipMemcpyDeviceToHost, s));
     }
     if (host_res || where == BB_HOST || (out_keys && res->where != BB_DEVICE)) BB_HIP(hipStreamSynchronize(s));
     return BB_OK;
@@ -1635,7 +1676,7 @@ int bb_set_option(bb_index* x, int32_t option, int64_t value) {
       x->lists_opt = (int)value;
       return BB_OK;
     case BB_OPT_SMALL_BATCH:
-      if (value < -1 || value > 2) return fail(BB_E_ARG, "BB_OPT_SMALL_BATCH must be -1, 0, 1 or 2");
+      if (value < -1 || value > 1) return fail(BB_E_ARG, "BB_OPT_SMALL_BATCH must be -1, 0 or 1");
       x->sq_opt = (int)value;
       return BB_OK;
     case BB_OPT_WORKSPACE_BYTES:

@@ -339,55 +339,6 @@ struct PrepArgs {
   int32_t q_perm;           // the bf16 operand in lane order, not row-major: 1 = scan4's (scan4_q_offset), 2 = scan2's
 };
 
-// Small-batch exact search (sq.hip): B <= kSqMaxB query rows of one side against an f32 index
-// in ONE pass over the f32 rows — every score exact (f32 products summed in f64 in
-// rescore_rows' fixed order, rounded to f32), no approximate scan and no re-rank.  Each
-// workgroup owns rows [blk·rpw, +rpw) and leaves per query its top kSqM keys, its present
-// maximum (rank 0) and the order images of all its rows (for overflowed lists); the merge —
-// its own launch, or the workgroup whose arrival on `ticket` comes last — turns them into the
-// exact top-K per query.
-constexpr int kSqMaxB = 16;
-constexpr int kSqMaxK = 128;    // internal list length (K_int) the merge sorts in registers
-constexpr int kSqM = 4;         // keys per workgroup list
-constexpr int kSqMaxRows = 256; // rows per workgroup
-constexpr int kSqMaxWg = 512;   // workgroups (8 lists per merge lane)
-constexpr int kSqCand = 256;    // merge candidates per query (beyond: the exact wave fallback)
-struct SqArgs {
-  const float* X;           // f32 rows [n][ldx], normalised, zero padded
-  int64_t ldx;
-  int32_t n;
-  uint32_t gid0;            // global id of row 0
-  const uint32_t* present;  // local-row bitsets: the side's item space,
-  const uint32_t* mask;     //   the constraint mask (null = all),
-  const uint32_t* excl;     //   per-query exclusions [B][excl_ld] (null = none)
-  int64_t excl_ld;
-  int32_t drop;             // keep the present maximum of each query (rank-0 drop)
-  int32_t B;
-  // queries: q_kind 0 = raw rows q_src (q_dtype, stride q_ld, width q_d) normalised as
-  // prep_kernel does (qnorm.h); 1 = the stored rows of ids q_ids (minus q_id_offset) of X;
-  // 2 = q_src rows as they are (CF user factors)
-  int32_t q_kind;
-  const void* q_src;
-  int32_t q_dtype;
-  int64_t q_ld;
-  int32_t q_d;
-  const int64_t* q_ids;
-  int64_t q_id_offset;
-  int32_t rpw, nwg;         // rows per workgroup (multiple of 4), workgroups
-  uint64_t* wg_top;         // [B][nwg][kSqM] keys (0 = empty)
-  uint64_t* wg_pmax;        // [B][nwg] present-maximum keys (drop)
-  uint32_t* ords;           // [B][ords_ld] order image per row, 0 = ineligible
-  int64_t ords_ld;
-  int32_t K;                // internal list length
-  int32_t k_final;          // final outputs (out_scores != null) ...
-  float* out_scores;
-  int64_t* out_ids;
-  int32_t* out_counts;
-  uint64_t* keys_out;       // ... or the key list [B][K] + max_out [B] (BB_Q_OUT_KEYS)
-  uint64_t* max_out;
-  unsigned long long* ticket;  // fused merge: arrival counter (monotonic), else null
-};
-
 struct MaskArgs {
   const int32_t* parts;
   const int16_t* year;
@@ -434,10 +385,6 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 // a key (ord << 32) in thr_out[row]; 0 (take every eligible item) when fewer than K exist
 hipError_t launch_pilot_bound(const uint32_t* top, int n_chunks, int m, int nb, int K, int B, uint64_t* thr_out,
                               hipStream_t s);
-// small-batch exact search: the row pass (+ the merge by the last workgroup when a.ticket is
-// set), and the separate merge launch otherwise
-hipError_t launch_sq_scan(const SqArgs& a, hipStream_t s);
-hipError_t launch_sq_merge(const SqArgs& a, hipStream_t s);
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s);
 hipError_t launch_prep2(const PrepArgs& a0, const PrepArgs& a1, hipStream_t s);
 hipError_t launch_mask(const MaskArgs& a, hipStream_t s);

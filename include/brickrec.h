@@ -201,12 +201,12 @@ int bb_get_profile(bb_index* idx, bb_profile* out);
  *                           keep bounded per-lane candidate lists in the scan instead of
  *                           writing a score image for the select (no B×n image).  Results are
  *                           identical either way.
- *   BB_OPT_SMALL_BATCH      -1 auto (default), 0 off, 1 on (merge as its own launch), 2 on
- *                           (merge in the last workgroup: one launch): batches of up to 16
- *                           query rows of one side (semantic / similar / CF) on an f32 index
- *                           of up to 131,072 rows take one exact pass over the f32 rows (every
- *                           score exact, no approximate scan or re-rank) — the reference's
- *                           one-query request shape.  Results are identical either way. */
+ *   BB_OPT_SMALL_BATCH      -1 auto (default, = 1), 0 off: batches of up to 16 query rows (any
+ *                           mode, hybrid included) on an f32 index of up to 65,536 rows take
+ *                           one approximate pass over the bf16 copy per side and an exact
+ *                           rescore of the candidates within its proven bound (no MFMA scan,
+ *                           lists or list select) — the reference's one-query request shape.
+ *                           Results are identical either way. */
 #define BB_OPT_STREAM 1
 #define BB_OPT_STREAM_MIN_ITEMS 2
 #define BB_OPT_WORKSPACE_BYTES 3

@@ -1,11 +1,26 @@
-# Final-evidence pass: bench.py line (with cpu_baseline) and rocprofv3 --kernel-trace --stats per workload.
+# Evidence pass on the GPU box: per workload the bench.py line (with cpu_baseline), then
+# rocprofv3 --kernel-trace --stats of `bench.py --inflight 1` — one batch at a time, so the
+# kernel averages are not inflated by other lanes' batches and match the bench line's
+# HIP-event kernel times (roofline.kernel_us) — then the FETCH_SIZE / WRITE_SIZE passes.
+#   bash tools/evidence_run.sh TAG [workloads...]      (default: c2 c3 c4 c5)
 set -e
-O=gpurun_out/${1:-r03h}; mkdir -p $O
+T=${1:-r04}; shift || true
+WL=${@:-c2 c3 c4 c5}
+O=gpurun_out/$T; mkdir -p $O
 R=$(pwd)
-for w in c2 c3 c4 c5; do
-  st=""
-  timeout -k 10 420 python3 bench.py --workload $w $st > $O/bench_$w.log 2>&1
+for w in $WL; do
+  timeout -k 10 420 python3 bench.py --workload $w > $O/bench_$w.log 2>&1
   tail -1 $O/bench_$w.log | cut -c1-300
-  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$O/prof_$w" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu --no-sweep --workload $w $st > "$R/$O/prof_$w.log" 2>&1 )
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$O/prof_$w" -o run \
+      --output-format csv -- python3 "$R/bench.py" --no-cpu --no-sweep --inflight 1 --workload $w > "$R/$O/prof_$w.log" 2>&1 )
   echo "prof $w ok"
+  i=0
+  for grp in FETCH_SIZE WRITE_SIZE; do
+    i=$((i+1))
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $grp -d "$R/$O/pmc_$w/p$i" -o run \
+        --output-format csv -- python3 "$R/bench.py" --steps 30 --warmup 5 --no-cpu --no-sweep --inflight 1 --workload $w \
+        > "$R/$O/pmc_${w}_p$i.log" 2>&1 )
+  done
+  python3 "$R/tools/pmc_summary.py" "$R/$O/pmc_$w" > "$R/$O/pmc_${w}_summary.json"
+  echo "pmc $w ok"
 done

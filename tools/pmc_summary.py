@@ -2,6 +2,7 @@
 plus `_dispatches` (how many dispatches of that kernel the run made, from the first counter
 seen)."""
 import csv
+import re
 import glob
 import json
 import sys
@@ -13,7 +14,8 @@ for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     with open(f) as fh:
         for row in csv.DictReader(fh):
             name = row.get("Kernel_Name", "")
-            short = name.split("(")[0].replace("void ", "")[:60]
+            # drop the parameter list only (names in anonymous namespaces hold "(" too)
+            short = re.sub(r"\([^()]*\)\s*$", "", name).replace("void ", "")[:80]
             out[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
 res = {}
 for k, d in out.items():

@@ -13,6 +13,7 @@ for v in "$@"; do
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print(sys.argv[1], round(d["value"] / 1e6, 3), d["p50_ms_serial"], d["kernels_us_per_step"],
-      [(s["B"], s["p50_ms_serial"], round(s["queries_per_s_inflight3"] / 1e6, 3)) for s in d["gpu_batch_sweep"]])
+      [(s["B"], s["p50_ms_serial"], round(s["queries_per_s_inflight3"] / 1e6, 3)) for s in d["gpu_batch_sweep"]],
+      d.get("request_latency", {}).get("p50_ms_serial"))
 PY
 done
