@@ -738,12 +738,16 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   const int sq_sel = x->sq_opt >= 0 ? x->sq_opt : sq_env;
   const bool sq_sides = (!need_content || (x->items_bf.p && x->Dpad <= kRrMaxD && x->d <= kRrMaxD && x->Dpad_b <= 512)) &&
                         (!need_cf || (x->cf_bf.p && x->Rpad <= kRrMaxD && x->r <= kRrMaxD && x->Rpad_b <= 512));
+  // rows per pass workgroup the LDS holds whole (both sides' widths)
+  const int sq_cap = !sq_sides ? 0
+                     : std::min(need_content ? sq_rows_cap(x->Dpad_b, std::min(B, kSqMaxB), x->Dpad) : kSqMaxRows,
+                                need_cf ? sq_rows_cap(x->Rpad_b, std::min(B, kSqMaxB), x->Rpad) : kSqMaxRows);
   if (sq_sel != 0 && x->dtype == F32 && B <= kSqMaxB && K_int <= kSqMaxK && sq_sides &&
-      x->n <= (int64_t)kSqMaxWg * kSqMaxRows) {
+      x->n <= (int64_t)kSqMaxWg * sq_cap) {
     static const int sq_wg_env = ab_env("BB_SQ_WG") ? atoi(ab_env("BB_SQ_WG")) : 256;
     const bool hyb = sides == 2;
     const int64_t wg_goal = std::max(1, std::min(sq_wg_env, kSqMaxWg));
-    const int32_t rpw = (int32_t)std::min<int64_t>(kSqMaxRows, std::max<int64_t>(4, round_up((x->n + wg_goal - 1) / wg_goal, 4)));
+    const int32_t rpw = (int32_t)std::min<int64_t>(sq_cap, std::max<int64_t>(4, round_up((x->n + wg_goal - 1) / wg_goal, 4)));
     const int32_t nwg = (int32_t)((x->n + rpw - 1) / rpw);
     const size_t top_side = (size_t)B * nwg * kSqM, ord_side = (size_t)B * x->n * 2;
     const size_t q_side = (size_t)B * kRrMaxD;
@@ -805,11 +809,50 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       }
       return a;
     };
-    const SqArgs a0 = side_args(0);
-    const SqArgs a1 = hyb ? side_args(1) : a0;
+    SqArgs a0 = side_args(0);
+    SqArgs a1 = hyb ? side_args(1) : a0;
+    // BB_SQ_TRACE (probe runs): phase stamps of side 0's pass workgroups and merge rows
+    static const bool sq_trace = ab_env("BB_SQ_TRACE") != nullptr;
+    if (sq_trace) {
+      if ((rc = x->trace.ensure((size_t)(nwg + B) * 8 * 8))) return rc;
+      BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)(nwg + B) * 64, s));
+      a0.trace = (uint64_t*)x->trace.p;
+      a0.mtrace = a0.trace + (size_t)nwg * 8;
+    }
     for (int side = 0; side < sides; ++side)
       if ((rc = timed(x, K_GEMM, s, [&] { return launch_sq_scan(side ? a1 : a0, s); }))) return rc;
     if ((rc = timed(x, K_SELECT, s, [&] { return launch_sq_merge(a0, hyb ? &a1 : nullptr, s); }))) return rc;
+    if (sq_trace) {
+      std::vector<uint64_t> tr((size_t)(nwg + B) * 8);
+      BB_HIP(hipMemcpyAsync(tr.data(), x->trace.p, tr.size() * 8, hipMemcpyDeviceToHost, s));
+      BB_HIP(hipStreamSynchronize(s));
+      uint64_t t0 = ~0ull, tend = 0;
+      double ph[5] = {0};
+      for (int w2 = 0; w2 < nwg; ++w2) {
+        const uint64_t* t = &tr[(size_t)w2 * 8];
+        t0 = std::min(t0, t[0]);
+        tend = std::max(tend, t[4]);
+        for (int j = 1; j < 5; ++j) ph[j] += (double)(t[j] - t[0]);
+      }
+      uint64_t s_max = 0;
+      for (int w2 = 0; w2 < nwg; ++w2) s_max = std::max<uint64_t>(s_max, tr[(size_t)w2 * 8] - t0);
+      double mp[4] = {0}, ce = 0, cp = 0;
+      uint64_t m0 = ~0ull, m1 = 0;
+      for (int bq = 0; bq < B; ++bq) {
+        const uint64_t* t = &tr[((size_t)nwg + bq) * 8];
+        m0 = std::min(m0, t[0]);
+        m1 = std::max(m1, t[3]);
+        for (int j = 1; j < 4; ++j) mp[j] += (double)(t[j] - t[0]);
+        ce += (double)(uint32_t)t[4];
+        cp += (double)(t[4] >> 32);
+      }
+      fprintf(stderr, "[bb sq trace] B=%d nwg=%d rpw=%d pass (us from workgroup start): loads-issued %.2f q-ready %.2f "
+              "rows-done %.2f end %.2f | starts spread %.2f, span %.2f | merge: gathered %.2f rescored %.2f end %.2f, "
+              "span %.2f, cands %.1f + r0 %.1f | pass end -> merge start %.2f\n",
+              B, nwg, rpw, ph[1] / nwg / 100, ph[2] / nwg / 100, ph[3] / nwg / 100, ph[4] / nwg / 100, (double)s_max / 100,
+              (double)(tend - t0) / 100, mp[1] / B / 100, mp[2] / B / 100, mp[3] / B / 100, (double)(m1 - m0) / 100, ce / B,
+              cp / B, ((double)m0 - (double)tend) / 100);
+    }
     if (out_keys) {
       const hipMemcpyKind kind = res->where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
       BB_HIP(hipMemcpyAsync(res->keys, x->keys.p, (size_t)sides * B * K_int * 8, kind, s));

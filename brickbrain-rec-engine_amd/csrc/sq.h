@@ -1,8 +1,8 @@
 // sq.h — small-batch exact search (sq.hip): the arguments shared by api.hip and the kernels.
 //
 // B <= kSqMaxB query rows of one side against an f32 index (that has its bf16 copy): ONE
-// approximate pass over the bf16 rows in f32 — every approximate score a within a proven δ
-// of the exact score s (the f32 products summed in f64 in rescore_rows' fixed order, rounded to
+// approximate pass over the bf16 rows on the matrix cores (bf16 rows x bf16 hi + lo query
+// split, f32 accumulation) — every approximate score a within a proven δ of the exact score s (the f32 products summed in f64 in rescore_rows' fixed order, rounded to
 // f32) — leaves per workgroup and query its top kSqM approximate keys (and present keys for the
 // rank-0 drop) and every row's approximate order image; the merge (one workgroup per query and
 // side) takes the candidates within 2δ of a lower bound of the K-th score, rescores exactly
@@ -58,7 +58,13 @@ struct SqArgs {
   int32_t* out_counts;
   uint64_t* keys_out;       // ... or the exact key list [B][K] + max_out [B] (BB_Q_OUT_KEYS, hybrid
   uint64_t* max_out;        //     sides; max_out null: not written)
+  uint64_t* trace;          // probe runs (BB_SQ_TRACE): pass phase stamps [nwg][8], or null
+  uint64_t* mtrace;         //   and merge phase stamps [B][8] of this side, or null
 };
+
+// rows per pass workgroup whose bf16 rows (ldb wide), B query rows (ldx wide) and order images
+// fit the LDS at once (a multiple of 16, <= kSqMaxRows)
+int sq_rows_cap(int64_t ldb, int B, int64_t ldx);
 
 // the approximate pass, then the merge (a1 != null: both hybrid sides in one launch)
 hipError_t launch_sq_scan(const SqArgs& a, hipStream_t s);

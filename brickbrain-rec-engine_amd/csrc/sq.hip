@@ -6,13 +6,12 @@
 // one liked set (:612-677).  For such batches the MFMA scan + per-lane lists + list select of
 // the large-batch path is mostly latency; here (sq.h):
 //
-//   pass   workgroup blk streams rows [blk·rpw, +rpw) of the bf16 copy through an LDS ring by
-//          LDS-DMA (all of a 25K-row index's block in flight at once) and scores them in f32
-//          against the f32 query rows (packed FMAs, 16 lanes per row): a = Σ x̃_j q_j.  With
-//          q unrounded, |a − s| <= δ = ‖q‖·(E_x + γ·Ñ_x + 2^-23·N_x) for the exact score s
-//          (Cauchy–Schwarz on Σ(x̃_j − x_j)q_j, the f32 summation bound γ = 2·ldb·2^-24, the f32
-//          rounding of s; E_x, N_x, Ñ_x = rr_stats).  Per query it leaves its top kSqM
-//          eligible (and present) approximate keys and every row's approximate order image.
+//   pass   workgroup blk stages rows [blk·rpw, +rpw) of the bf16 copy into LDS by LDS-DMA
+//          (the whole block in flight at once) and scores them on the matrix cores against the
+//          query rows split into bf16 hi + lo (16 queries per MFMA column block, f32
+//          accumulation): a = Σ x̃_j (h_j + l_j).  |a − s| <= δ (sq_margin) for the exact score s
+//          (E_x, N_x, Ñ_x = rr_stats).  Per query it leaves its top kSqM eligible (and present)
+//          approximate keys and every row's approximate order image.
 //   merge  one workgroup per query: L = a lower bound of the K-th largest workgroup maximum
 //          (16-bit prefix search: K distinct items reach it, so the exact K-th score is
 //          >= L − δ and every exact top-K member has a >= L − 2δ); the candidates are the list
@@ -32,7 +31,6 @@ namespace {
 
 constexpr int kSqThreads = 256;
 constexpr int kSqWaves = kSqThreads / 64;
-typedef float f2v __attribute__((ext_vector_type(2)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
 // 16 B of LDS as four u32 (bf16 pairs).  (Read as a float vector, __builtin_bit_cast of its
@@ -43,7 +41,6 @@ __device__ __forceinline__ u4v lds_u4(const void* p, int c) {
                                                          c * 16);
 }
 
-__device__ __forceinline__ bool bit_of(const uint32_t* w, int i) { return (w[i >> 5] >> (i & 31)) & 1u; }
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
@@ -51,19 +48,6 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     const uint64_t y = __shfl_xor(v, o);
     v = v > y ? v : y;
   }
-  return v;
-}
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_f32(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-// sum over the 16 lanes of a DPP row (the approximate score: any order)
-__device__ __forceinline__ float sum16_f32(float v) {
-  v += dpp_f32<0xB1>(v);
-  v += dpp_f32<0x4E>(v);
-  v += dpp_f32<0x141>(v);
-  v += dpp_f32<0x140>(v);
   return v;
 }
 
@@ -134,163 +118,185 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
 }
-// this wave's LDS-DMA of the chunk to read has landed when at most N of its pieces are
-// outstanding; then every wave's (one statement with the barrier: no memory access moves
-// across it)
-template <int N>
-__device__ __forceinline__ void wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+// wave maximum of a u32 (uniform result): DPP within each 16-lane row, readlane across rows
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, dpp_u32<0xB1>(v));
+  v = max(v, dpp_u32<0x4E>(v));
+  v = max(v, dpp_u32<0x141>(v));
+  v = max(v, dpp_u32<0x140>(v));
+  const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16),
+                 c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return max(max(a, b), max(c, d));
 }
 
-// Ring chunks of the pass (16 bf16 rows of up to 128·CPB elements = 4·CPB KiB each): the
-// prologue puts NBUF-1 of them in flight (a 25,216 x 384 index's 99-row block is 7 chunks)
-template <int CPB, int RS>
-constexpr int sq_nbuf() { return CPB >= 4 ? 6 : CPB == 3 ? (RS >= 2 ? 10 : 8) : 10; }
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+// eight f32 -> bf16 (round to nearest even) packed as the MFMA operand
+__device__ __forceinline__ u4v pack_bf16x8(const float (&v)[8]) {
+  u4v r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = (uint32_t)to_bf16(v[2 * i]) | ((uint32_t)to_bf16(v[2 * i + 1]) << 16);
+  return r;
+}
 
-// Approximate pass.  Lane (g, p): 16-lane group g = 4 slots per wave, p its chunk lane (16-B
-// chunks of 8 bf16 elements p, p+16, ...).  Slot g takes row slot g % RS of the wave's RS rows
-// and query set g / RS (QPW queries); a wave covers QW = (4/RS)·QPW queries, and with more
-// queries than that the waves split into nqg query groups (kSqWaves / nqg row phases each).
-// The only vector-memory operations of the row loop are the ring's DMAs (counted by vmcnt);
-// eligibility is applied after the loop.
-template <int CPB, int RS, int QPW>
+// Approximate pass on the matrix cores.  The workgroup's rows are staged into LDS by LDS-DMA
+// (the whole block in flight at once, one wait) in a chunk-major image: 16-row chunks, and in
+// a chunk the 16-B column cc of row r at slot cc·16 + r — one 1-KiB LDS-DMA piece (64 slots) per
+// four columns, and the MFMA operand of a 32-wide k-step is one contiguous, conflict-free
+// 1-KiB wave read.  Each wave scores whole chunks: per k-step two v_mfma_f32_16x16x32_bf16 —
+// the bf16 rows (A: 16 rows x 32) against the query rows split into bf16 hi + lo (B: 32 x 16
+// queries, up to 16 per launch; q − hi − lo <= 2^-18·|q|), f32 accumulation.  KS = ldb / 32.
+template <int KS>
 __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
-  constexpr int QW = (4 / RS) * QPW;
-  constexpr int NBUF = sq_nbuf<CPB, RS>();
-  constexpr int CHB = 4096 * CPB;
   extern __shared__ __attribute__((aligned(16))) char sq_smem[];
   const int B = a.B;
-  const int ldb = (int)a.ldb, nchb = ldb >> 3, ldx = (int)a.ldx;
-  char* ring = sq_smem;
-  float* qs = (float*)(sq_smem + NBUF * CHB);  // [B][ldx] f32 query rows
-  uint32_t* sel = (uint32_t*)(qs + B * ldx);   // [B][rpw] approximate order images
+  const int ldb = (int)a.ldb, ldx = (int)a.ldx;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int p = lane & 15, g = lane >> 4;
-  const int rs = g % RS, qsub = g / RS;
-  const int nqg = (B + QW - 1) / QW;
-  const int qg = w % nqg, ph = w / nqg, nph = kSqWaves / nqg;
   const int blk = blockIdx.x;
   const int r0 = blk * a.rpw, r1 = min(a.n, r0 + a.rpw), nr = r1 - r0;
   const int nck = (nr + 15) >> 4;
-  const char* Xb = (const char*)a.Xb + (size_t)r0 * ldb * 2;  // the block
-  const int blk_bytes = nr * ldb * 2;
-  const uint32_t ring_lds = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)ring);
-  auto stage = [&](int c) __attribute__((always_inline)) {
-    const uint32_t dst0 = ring_lds + (uint32_t)((c % NBUF) * CHB);
-#pragma unroll
-    for (int i = 0; i < CPB; ++i) {
-      const int piece = w + 4 * i;
-      const int off = c * 32 * ldb + piece * 1024 + lane * 16;  // byte offset in the block
-      glds16(Xb + (off < blk_bytes ? off : 0), __builtin_amdgcn_readfirstlane(dst0 + piece * 1024));
-    }
+  constexpr int CHB = 32 * 32 * KS;                   // bytes of a 16-row chunk (16 · ldb · 2)
+  char* rows = sq_smem;                               // [nck][CHB]
+  float* qs = (float*)(sq_smem + (size_t)nck * CHB);  // [B][ldx] f32 query rows
+  uint32_t* sel = (uint32_t*)(qs + B * ldx);          // [B][rpw] approximate order images
+  auto stamp = [&](int slot) {  // BB_SQ_TRACE probe runs: phase timeline (100 MHz), 8 words per workgroup
+    if (a.trace && tid == 0) a.trace[(size_t)blk * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
-#pragma unroll
-  for (int c = 0; c < NBUF - 1; ++c)
-    if (c < nck) stage(c);
+  stamp(0);
+  {
+    const uint32_t rows_lds = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)rows);
+    const int r = lane & 15;
+    for (int c = 0; c < nck; ++c) {
+      const int row = 16 * c + r < nr ? r0 + 16 * c + r : r0;  // rows past the block: any valid row
+      const char* src_row = (const char*)a.Xb + (size_t)row * ldb * 2;
+      for (int P = w; P < KS; P += kSqWaves) {  // wave-uniform
+        const int cc = 4 * P + (lane >> 4);
+        glds16(src_row + cc * 16, __builtin_amdgcn_readfirstlane(rows_lds + (uint32_t)(c * CHB + P * 1024)));
+      }
+    }
+  }
 
   // query rows, as prep_kernel writes its f32 operand: normalised raw rows (qnorm.h), the
-  // stored rows of item ids, or CF rows as they are; zero past the row.  Workgroup 0 also
-  // hands them to the merge (q_out).
-  for (int b = w; b < B; b += kSqWaves) {
-    float v[kQnC];
-    if (a.q_kind == 1) {  // (all loads of the row in flight together, as load_chunk)
+  // stored rows of item ids, or CF rows as they are; zero past the row.  A wave's rows
+  // (b = w, w + 4, ...) are all loaded before any is used: one round trip, not one per row.
+  // Workgroup 0 also hands them to the merge (q_out).
+  constexpr int QT = kSqMaxB / kSqWaves;
+  double xq[QT][kQnC];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int b = w + kSqWaves * t;
+    if (b >= B) break;  // wave-uniform
+    if (a.q_kind == 1) {
       const int64_t id = a.q_ids[b] - a.q_id_offset;
       const bool ok = id >= 0 && id < a.n;
       const float* src = a.X + (size_t)(ok ? id : 0) * ldx;
+      float v[kQnC];
 #pragma unroll
       for (int c = 0; c < kQnC; ++c) v[c] = src[min(lane + 64 * c, ldx - 1)];
 #pragma unroll
-      for (int c = 0; c < kQnC; ++c) v[c] = ok ? v[c] : 0.f;
+      for (int c = 0; c < kQnC; ++c) xq[t][c] = ok && lane + 64 * c < ldx ? (double)v[c] : 0.0;
     } else {
-      double xq[kQnC];
-      load_chunk<kQnC>(a.q_src, a.q_dtype, (size_t)b * a.q_ld, 0, a.q_d, lane, xq);
-      const double nrm = a.q_kind == 0 ? qn_norm(xq) : 1.0;
-#pragma unroll
-      for (int c = 0; c < kQnC; ++c) v[c] = qn_elem(xq[c], nrm);
+      load_chunk<kQnC>(a.q_src, a.q_dtype, (size_t)b * a.q_ld, 0, a.q_d, lane, xq[t]);
     }
+  }
+  stamp(1);
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int b = w + kSqWaves * t;
+    if (b >= B) break;
+    const double nrm = a.q_kind == 0 ? qn_norm(xq[t]) : 1.0;
 #pragma unroll
     for (int c = 0; c < kQnC; ++c) {
       const int i = lane + 64 * c;
       if (i < ldx) {
-        qs[b * ldx + i] = v[c];
-        if (blk == 0) a.q_out[(size_t)b * ldx + i] = v[c];
+        const float v = qn_elem(xq[t][c], nrm);
+        qs[b * ldx + i] = v;
+        if (blk == 0) a.q_out[(size_t)b * ldx + i] = v;
       }
     }
   }
-  __syncthreads();  // (its vmcnt(0) also lands the prologue's chunks)
-  f2v qf[QPW][CPB][4];
-  int qb[QPW];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows' LDS-DMA has landed
+  __syncthreads();
+  stamp(2);
+  // the B operand: lane l holds query n = l & 15, k = 32·ks + 8·(l >> 4) + j, as bf16 hi + lo
+  u4v qhi[KS], qlo[KS];
+  {
+    const int n = lane & 15;
 #pragma unroll
-  for (int i = 0; i < QPW; ++i) {
-    qb[i] = qg * QW + qsub * QPW + i;
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k0 = 32 * ks + 8 * (lane >> 4);
+      const bool on = n < B && k0 < ldx;
+      const f4v v0 = on ? lds_f4(qs + n * ldx, k0 >> 2) : f4v{0.f, 0.f, 0.f, 0.f};
+      const f4v v1 = on ? lds_f4(qs + n * ldx, (k0 >> 2) + 1) : f4v{0.f, 0.f, 0.f, 0.f};
+      float h[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w}, l[8];
+      qhi[ks] = pack_bf16x8(h);
 #pragma unroll
-    for (int j = 0; j < CPB; ++j) {
-      const int c = p + 16 * j;
-      const bool on = qb[i] < B && c < nchb && 8 * c < ldx;
-      const f4v v0 = on ? lds_f4(qs + qb[i] * ldx, 2 * c) : f4v{0.f, 0.f, 0.f, 0.f};
-      const f4v v1 = on ? lds_f4(qs + qb[i] * ldx, 2 * c + 1) : f4v{0.f, 0.f, 0.f, 0.f};
-      qf[i][j][0] = f2v{v0.x, v0.y};
-      qf[i][j][1] = f2v{v0.z, v0.w};
-      qf[i][j][2] = f2v{v1.x, v1.y};
-      qf[i][j][3] = f2v{v1.z, v1.w};
+      for (int j = 0; j < 8; ++j) {
+        const float hb = __uint_as_float((uint32_t)to_bf16(h[j]) << 16);
+        l[j] = h[j] - hb;  // exact (the f32 residual of the bf16 rounding)
+      }
+      qlo[ks] = pack_bf16x8(l);
     }
   }
-
-  for (int c = 0; c < nck; ++c) {
-    const int ahead = min(nck - 1 - c, NBUF - 2);
-    switch (ahead) {
-      case 0: wait_barrier<0>(); break;
-      case 1: wait_barrier<CPB>(); break;
-      case 2: wait_barrier<2 * CPB>(); break;
-      case 3: wait_barrier<3 * CPB>(); break;
-      case 4: wait_barrier<4 * CPB>(); break;
-      case 5: wait_barrier<5 * CPB>(); break;
-      case 6: wait_barrier<6 * CPB>(); break;
-      case 7: wait_barrier<7 * CPB>(); break;
-      default: wait_barrier<8 * CPB>(); break;
+  for (int c = w; c < nck; c += kSqWaves) {  // wave-uniform
+    const char* chunk = rows + c * CHB;
+    u4v af[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) af[ks] = lds_u4(chunk, ks * 64 + lane);
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[ks]), __builtin_bit_cast(bf16x8, qhi[ks]),
+                                                    acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[ks]), __builtin_bit_cast(bf16x8, qlo[ks]),
+                                                    acc, 0, 0, 0);
     }
-    // refill the buffer read in the previous phase (every wave has passed this barrier, its
-    // reads consumed)
-    if (c + NBUF - 1 < nck) stage(c + NBUF - 1);
-    const char* buf = ring + (c % NBUF) * CHB;
-    const int rows_c = min(16, nr - 16 * c);
-    for (int s0 = ph * RS; s0 < 16; s0 += nph * RS) {  // wave-uniform
-      const int ri = s0 + rs;
-      const char* xr = buf + (ri < rows_c ? ri : 0) * ldb * 2;
-      f2v acc[QPW];
+    const int n = lane & 15, rb = 16 * c + 4 * (lane >> 4);  // D: query n, rows rb .. rb + 3
+    if (n < B) {
 #pragma unroll
-      for (int i = 0; i < QPW; ++i) acc[i] = f2v{0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < CPB; ++j) {
-        const u4v raw = lds_u4(xr, min(p + 16 * j, nchb - 1));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t u = raw[k];
-          const f2v xv = f2v{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
-#pragma unroll
-          for (int i = 0; i < QPW; ++i) acc[i] = __builtin_elementwise_fma(xv, qf[i][j][k], acc[i]);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < QPW; ++i) {
-        const float s = sum16_f32(acc[i].x + acc[i].y);
-        if (p == 0 && ri < rows_c && qb[i] < B) sel[qb[i] * a.rpw + 16 * c + ri] = ord_of(s + 0.0f);
-      }
+      for (int i = 0; i < 4; ++i)
+        if (rb + i < nr) sel[n * a.rpw + rb + i] = ord_of(acc[i] + 0.0f);
     }
   }
   __syncthreads();
+  stamp(3);
 
   // per query: eligibility, the order images of the rows, the top kSqM eligible (and present)
-  // approximate keys
-  for (int b = w; b < B; b += kSqWaves) {
-    uint32_t o[kSqMaxRows / 64], op[kSqMaxRows / 64];
-    const uint32_t* exb = a.excl ? a.excl + (size_t)b * a.excl_ld : nullptr;
+  // approximate keys.  The item-space and mask words are the same for every query: loaded once;
+  // a wave's exclusion words for all its queries in one round.
+  constexpr int NE = kSqMaxRows / 64;
+  uint32_t wp[NE], wm[NE], wx[QT][NE];
 #pragma unroll
-    for (int e = 0; e < kSqMaxRows / 64; ++e) {
+  for (int e = 0; e < NE; ++e) {
+    const int row = min(r0 + lane + 64 * e, a.n - 1);
+    wp[e] = a.present[row >> 5];
+    wm[e] = a.mask ? a.mask[row >> 5] : 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int b = w + kSqWaves * t;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int row = min(r0 + lane + 64 * e, a.n - 1);
+      wx[t][e] = a.excl && b < B ? a.excl[(size_t)b * a.excl_ld + (row >> 5)] : 0u;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int b = w + kSqWaves * t;
+    if (b >= B) break;  // wave-uniform
+    uint32_t o[NE], op[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
       const int i = lane + 64 * e, row = r0 + i;
       const uint32_t raw = i < nr ? sel[b * a.rpw + i] : 0u;
-      const bool pres = i < nr && bit_of(a.present, row);
-      const bool elig = pres && (!a.mask || bit_of(a.mask, row)) && (!exb || !bit_of(exb, row));
+      const uint32_t bit = 1u << (row & 31);
+      const bool pres = i < nr && (wp[e] & bit);
+      const bool elig = pres && (wm[e] & bit) && !(wx[t][e] & bit);
       o[e] = elig ? raw : 0u;
       op[e] = a.drop && pres ? raw : 0u;
       if (i < nr) {
@@ -299,38 +305,63 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
       }
     }
     for (int set = 0; set < (a.drop ? 2 : 1); ++set) {  // wave-uniform
-      uint32_t(&oo)[kSqMaxRows / 64] = set ? op : o;
+      uint32_t(&oo)[NE] = set ? op : o;
       uint64_t mine = 0;
 #pragma unroll
-      for (int t = 0; t < kSqM; ++t) {
-        uint64_t best = 0;
+      for (int tt = 0; tt < kSqM; ++tt) {
+        // the largest remaining order image; among equal ones the lowest row (largest key)
+        uint32_t lm = 0;
 #pragma unroll
-        for (int e = 0; e < kSqMaxRows / 64; ++e) {
-          const uint64_t k = oo[e] ? make_key(oo[e], a.gid0 + (uint32_t)(r0 + lane + 64 * e)) : 0ull;
-          best = best > k ? best : k;
+        for (int e = 0; e < NE; ++e) lm = max(lm, oo[e]);
+        const uint32_t m = wave_max_u32(lm);
+        uint64_t key = 0;
+        if (m) {
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const uint64_t hit = __ballot(oo[e] == m);
+            if (hit && !key) {
+              const int src = __ffsll((unsigned long long)hit) - 1;
+              key = make_key(m, a.gid0 + (uint32_t)(r0 + src + 64 * e));
+              if (lane == src) oo[e] = 0u;
+            }
+          }
         }
-        best = wave_max_u64(best);
-#pragma unroll
-        for (int e = 0; e < kSqMaxRows / 64; ++e)
-          if (oo[e] && make_key(oo[e], a.gid0 + (uint32_t)(r0 + lane + 64 * e)) == best) oo[e] = 0u;
-        if (lane == t) mine = best;
+        if (lane == tt) mine = key;
       }
       if (lane < kSqM) (set ? a.wg_ptop : a.wg_top)[((size_t)b * a.nwg + blk) * kSqM + lane] = mine;
     }
   }
+  stamp(4);
 }
 
-template <int CPB, int RS>
-size_t sq_lds_bytes(const SqArgs& a) {
-  return (size_t)sq_nbuf<CPB, RS>() * 4096 * CPB + (size_t)a.B * a.ldx * 4 + (size_t)a.B * a.rpw * 4;
+// the re-rank margin 2δ (rr_margin) of a query row, every lane of the wave (qrow: the f32 row,
+// ldx wide):  δ = ‖q‖·(E_x + (γ + 2^-17)·Ñ_x + 2^-23·N_x) — Cauchy–Schwarz on Σ(x̃_j − x_j)q_j
+// (E_x), the hi + lo split residual |q − h − l| <= 2^-18·|q| against x̃ (2^-17·Ñ_x, with room),
+// the f32 accumulation of the 2·ldb exact bf16 products whatever the matrix core's order,
+// rounding or truncation (γ = 8·ldb·2^-24 >= (2·ldb)·2^-23 · Σ|h|+|l| / ‖q‖, with room), and
+// the f32 rounding of s (2^-23·N_x)
+__device__ __forceinline__ float sq_margin(const SqArgs& a, const float* qrow) {
+  const int lane = threadIdx.x & 63, ldx = (int)a.ldx;
+  float v[kQnC];
+#pragma unroll
+  for (int c = 0; c < kQnC; ++c) v[c] = qrow[min(lane + 64 * c, ldx - 1)];
+  double ss = 0.0;
+#pragma unroll
+  for (int c = 0; c < kQnC; ++c) ss = fma(lane + 64 * c < ldx ? (double)v[c] : 0.0, (double)v[c], ss);
+  ss = qn_wave_sum(ss);
+  const double qn = sqrt(ss) * (1.0 + 0x1p-40);
+  const double gam = (double)a.ldb * 0x1p-21 + 0x1p-17;
+  const double d = qn * ((double)a.stats[0] + gam * (double)a.stats[2] + 0x1p-23 * (double)a.stats[1]);
+  return rr_margin(__double2float_ru(d * (1.0 + 0x1p-20)));
 }
 
 // Candidates of one query by one wave from the workgroups' lists of kSqM approximate keys
 // (tops: [nwg][kSqM]): the bound is the K-th largest list maximum's 16-bit prefix (kth) or
-// the largest maximum (rank 0), minus the margin; the candidates are the list keys at or
-// above it, plus every row of a workgroup whose kSqM-th key reaches it that its list did not
-// hold.  Returns the count (it may exceed cap: the caller's slow path) and the bound.
-__device__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint32_t* ords, int K, float margin,
+// the largest maximum (rank 0), minus the margin (computed here from qrow while the list loads
+// are in flight); the candidates are the list keys at or above it, plus every row of a
+// workgroup whose kSqM-th key reaches it that its list did not hold.  Returns the count (it
+// may exceed cap: the caller's slow path) and the bound.
+__device__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint32_t* ords, int K, const float* qrow,
                               bool kth, uint64_t* cb, uint32_t cap, uint32_t* T_out) {
   const int lane = threadIdx.x & 63;
   const int nwg = a.nwg;
@@ -342,6 +373,7 @@ __device__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint3
 #pragma unroll
     for (int j = 0; j < kSqM; ++j) ent[i][j] = t < nwg ? tops[(size_t)t * kSqM + j] : 0ull;
   }
+  const float margin = sq_margin(a, qrow);
   uint32_t top;
   if (kth) {  // the largest multiple of 2^16 with >= K workgroup maxima at or above it
     uint32_t prefix = 0;
@@ -386,14 +418,21 @@ __device__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint3
 }
 
 // rescore keys[0..m) in place: exact keys (rescore_rows: the f32 rows, f64 sums in one fixed
-// order, rounded to f32); all kSqThreads threads
+// order, rounded to f32); all kSqThreads threads, 4 rows in flight per 16-lane group at d = 384
+// (the merge's ~K candidates in one round of gathers)
 __device__ __forceinline__ void sq_rescore(const SqArgs& a, uint64_t* keys, int m, const float* qs) {
   SelectArgs sa{};
   sa.rr_x = a.X;
   sa.rr_ld = a.ldx;
   sa.rr_d = (int)a.ldx;
   sa.rr_gid_base = a.gid0;
-  rr_rescore_any(keys, m, sa, qs);
+  const int cpl = (((int)a.ldx >> 2) + 15) >> 4;
+  const int t = threadIdx.x;
+  if (cpl <= 1) rescore_rows<1, 12, 16>(keys, m, sa, qs, t);
+  else if (cpl <= 2) rescore_rows<2, 8, 16>(keys, m, sa, qs, t);
+  else if (cpl <= 4) rescore_rows<4, 4, 16>(keys, m, sa, qs, t);
+  else if (cpl <= 6) rescore_rows<6, 4, 16>(keys, m, sa, qs, t);
+  else rescore_rows<8, 2, 16>(keys, m, sa, qs, t);
 }
 
 // Slow exact path (more candidates than the buffers hold: masses of equal scores): every
@@ -455,45 +494,31 @@ __global__ __launch_bounds__(kSqThreads) void sq_merge_kernel(SqArgs a0, SqArgs 
   __shared__ uint64_t run[kSqMaxK];
   __shared__ uint32_t scan_sh[kSelectThreads / 64];
   __shared__ uint32_t misc[8];
-  __shared__ float margin_sh;
   const int side = (int)blockIdx.x >= a0.B ? 1 : 0;
   const SqArgs& a = side ? a1 : a0;
   const int b = (int)blockIdx.x - side * a0.B;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int ldx = (int)a.ldx;
   const float* qrow = a.q_out + (size_t)b * ldx;
+  auto stamp = [&](int slot) {  // BB_SQ_TRACE probe runs: phase timeline (100 MHz)
+    if (a.mtrace && tid == 0) a.mtrace[(size_t)b * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   for (int i = tid; i < ldx; i += kSqThreads) qs[i] = qrow[i];
-  if (w == 0) {  // the bound δ of |approximate − exact| from the query's norm and the row statistics
-    double ss = 0.0;
-#pragma unroll
-    for (int c = 0; c < kQnC; ++c) {
-      const int i = lane + 64 * c;
-      const double v = (double)qrow[min(i, ldx - 1)];
-      ss = fma(i < ldx ? v : 0.0, v, ss);
-    }
-    ss = qn_wave_sum(ss);
-    if (lane == 0) {
-      const double qn = sqrt(ss) * (1.0 + 0x1p-40);
-      const double gam = 2.0 * (double)a.ldb * 0x1p-24;
-      const double d = qn * ((double)a.stats[0] + gam * (double)a.stats[2] + 0x1p-23 * (double)a.stats[1]);
-      margin_sh = rr_margin(__double2float_ru(d * (1.0 + 0x1p-20)));
-    }
-  }
-  __syncthreads();
-  const float margin = margin_sh;
   if (w == 0) {
     uint32_t T;
-    const uint32_t ce = sq_gather(a, a.wg_top + (size_t)b * a.nwg * kSqM, a.ords + (size_t)b * a.ords_ld, a.K, margin,
+    const uint32_t ce = sq_gather(a, a.wg_top + (size_t)b * a.nwg * kSqM, a.ords + (size_t)b * a.ords_ld, a.K, qrow,
                                   true, cand, kSqCand, &T);
     if (lane == 0) misc[0] = ce, misc[2] = T;
   } else if (w == 1) {
     uint32_t T = 0xFFFFFFFFu, cp = 0;
     if (a.drop)
-      cp = sq_gather(a, a.wg_ptop + (size_t)b * a.nwg * kSqM, a.ords_p + (size_t)b * a.ords_ld, 1, margin, false, ptmp,
+      cp = sq_gather(a, a.wg_ptop + (size_t)b * a.nwg * kSqM, a.ords_p + (size_t)b * a.ords_ld, 1, qrow, false, ptmp,
                      kSqPCand, &T);
     if (lane == 0) misc[1] = cp, misc[3] = T;
   }
   __syncthreads();
+  stamp(1);
   const uint32_t ce = misc[0], cp = misc[1];
   if (ce > (uint32_t)kSqCand || cp > (uint32_t)kSqPCand) {
     const uint32_t Te = misc[2], Tp = misc[3];
@@ -505,41 +530,42 @@ __global__ __launch_bounds__(kSqThreads) void sq_merge_kernel(SqArgs a0, SqArgs 
   __syncthreads();
   sq_rescore(a, cand, (int)(ce + cp), qs);
   __syncthreads();
+  stamp(2);
   if (w == 0) {
     uint64_t gm = 0;
     for (int i = lane; i < (int)cp; i += 64) gm = gm > cand[ce + i] ? gm : cand[ce + i];
     gm = wave_max_u64(gm);
     sq_emit_any(a, b, cand, (int)ce, gm);
+    if (a.mtrace && lane == 0) a.mtrace[(size_t)b * 8 + 4] = ce | ((uint64_t)cp << 32);
   }
+  stamp(3);
 }
 
-template <int CPB, int RS, int QPW>
-hipError_t launch_sq3(const SqArgs& a, hipStream_t s) {
-  const size_t lds = sq_lds_bytes<CPB, RS>(a);
+template <int KS>
+hipError_t launch_sq_ks(const SqArgs& a, hipStream_t s) {
+  const int nck = (a.rpw + 15) / 16;
+  const size_t lds = (size_t)nck * 32 * 32 * KS + (size_t)a.B * a.ldx * 4 + (size_t)a.B * a.rpw * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   // dynamic LDS beyond 64 KiB needs the per-kernel opt-in, at the size launched (grows only)
   static size_t allowed = 64 * 1024;
   if (lds > allowed) {
-    const hipError_t e = hipFuncSetAttribute((const void*)sq_scan_kernel<CPB, RS, QPW>,
+    const hipError_t e = hipFuncSetAttribute((const void*)sq_scan_kernel<KS>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     allowed = lds;
   }
-  hipLaunchKernelGGL((sq_scan_kernel<CPB, RS, QPW>), dim3(a.nwg), dim3(kSqThreads), lds, s, a);
+  hipLaunchKernelGGL(sq_scan_kernel<KS>, dim3(a.nwg), dim3(kSqThreads), lds, s, a);
   return hipGetLastError();
 }
 
-template <int CPB>
-hipError_t launch_sq2(const SqArgs& a, hipStream_t s) {
-  // (RS, QPW) by batch: 4 rows x 1 query, 4 x 2, 2 x 2 (x 2 query sets), 1 x 2 (x 4 sets;
-  // two query groups of waves above 8 queries)
-  if (a.B == 1) return launch_sq3<CPB, 4, 1>(a, s);
-  if (a.B == 2) return launch_sq3<CPB, 4, 2>(a, s);
-  if (a.B <= 4) return launch_sq3<CPB, 2, 2>(a, s);
-  return launch_sq3<CPB, 1, 2>(a, s);
-}
-
 }  // namespace
+
+int sq_rows_cap(int64_t ldb, int B, int64_t ldx) {
+  const int64_t avail = 160 * 1024 - (int64_t)B * ldx * 4;
+  int rows = kSqMaxRows;
+  while (rows > 16 && (int64_t)(rows / 16) * 32 * ldb + (int64_t)B * rows * 4 > avail) rows -= 16;
+  return rows;
+}
 
 hipError_t launch_sq_scan(const SqArgs& a, hipStream_t s) {
   if (a.B < 1 || a.B > kSqMaxB || a.ldx > kRrMaxD || (a.ldx & 31) || a.ldb < a.ldx || (a.ldb & 63) || a.ldb > 512 ||
@@ -547,11 +573,17 @@ hipError_t launch_sq_scan(const SqArgs& a, hipStream_t s) {
       (int64_t)a.nwg * a.rpw < a.n || (int64_t)(a.nwg - 1) * a.rpw >= a.n || a.n < 1 || a.ords_ld < a.n ||
       !a.present || !a.Xb || !a.X || !a.stats || !a.q_out || (a.drop && (!a.ords_p || !a.wg_ptop)))
     return hipErrorInvalidValue;
-  const int cpb = (int)((a.ldb + 127) / 128);
-  if (cpb <= 1) return launch_sq2<1>(a, s);
-  if (cpb <= 2) return launch_sq2<2>(a, s);
-  if (cpb <= 3) return launch_sq2<3>(a, s);
-  return launch_sq2<4>(a, s);
+  switch (a.ldb / 32) {
+    case 2: return launch_sq_ks<2>(a, s);
+    case 4: return launch_sq_ks<4>(a, s);
+    case 6: return launch_sq_ks<6>(a, s);
+    case 8: return launch_sq_ks<8>(a, s);
+    case 10: return launch_sq_ks<10>(a, s);
+    case 12: return launch_sq_ks<12>(a, s);
+    case 14: return launch_sq_ks<14>(a, s);
+    case 16: return launch_sq_ks<16>(a, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_sq_merge(const SqArgs& a0, const SqArgs* a1, hipStream_t s) {
