@@ -762,6 +762,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     float* f_sc = host_res ? (float*)x->out_sc.p : res->scores;
     int64_t* f_id = host_res ? (int64_t*)x->out_id.p : res->ids;
     int32_t* f_cnt = host_res ? (int32_t*)x->out_cnt.p : res->counts;
+    static const int sq_mopt = ab_env("BB_SQ_MOPT") ? atoi(ab_env("BB_SQ_MOPT")) : 3;
     // one side's pass: the content side (semantic / similar / hybrid side 0) or the CF side
     auto side_args = [&](int side) {
       const bool cf_side = q->mode == BB_MODE_CF || side == 1;
@@ -793,6 +794,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       a.rpw = rpw;
       a.nwg = nwg;
       a.K = K_int;
+      a.mopt = sq_mopt;
       a.wg_top = (uint64_t*)x->sq_top.p + side * top_side;
       a.wg_ptop = (uint64_t*)x->sq_ptop.p;  // (the rank-0 side only)
       a.ords = (uint32_t*)x->sq_ords.p + side * ord_side;

@@ -58,6 +58,7 @@ struct SqArgs {
   int32_t* out_counts;
   uint64_t* keys_out;       // ... or the exact key list [B][K] + max_out [B] (BB_Q_OUT_KEYS, hybrid
   uint64_t* max_out;        //     sides; max_out null: not written)
+  int32_t mopt;             // merge variants (BB_SQ_MOPT A/B runs; default 3): 1 = lists by nwg, early exit; 2 = rank emission
   uint64_t* trace;          // probe runs (BB_SQ_TRACE): pass phase stamps [nwg][8], or null
   uint64_t* mtrace;         //   and merge phase stamps [B][8] of this side, or null
 };

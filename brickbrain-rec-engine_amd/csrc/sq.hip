@@ -105,8 +105,47 @@ __device__ __forceinline__ void sq_emit(const SqArgs& a, int b, const uint64_t* 
   if (lane == 0 && a.max_out) a.max_out[b] = a.drop ? gmax : 0ull;
 }
 
+// The same result for C <= 64 keys without a sorting network: the keys are distinct (ids), so
+// lane l's rank is the number of larger keys, counted against each key broadcast in turn.
+__device__ __forceinline__ void sq_emit_rank(const SqArgs& a, int b, const uint64_t* cb, int C, uint64_t gmax) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t v = lane < C ? cb[lane] : 0ull;
+  const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
+  int r = 0;
+  for (int j = 0; j < C; ++j) {  // uniform
+    const uint64_t y = ((uint64_t)__builtin_amdgcn_readlane(vhi, j) << 32) | __builtin_amdgcn_readlane(vlo, j);
+    r += y > v;
+  }
+  const bool on = lane < C;
+  const int cnt = C < a.K ? C : a.K;
+  if (a.out_scores) {
+    const uint64_t h = __ballot(on && r == 0);
+    const uint64_t head = h ? __shfl(v, __ffsll((unsigned long long)h) - 1) : 0ull;
+    const int start = (gmax && cnt && head == gmax) ? 1 : 0;
+    const int c = min(a.k_final, cnt - start);
+    float* sc = a.out_scores + (size_t)b * a.k_final;
+    int64_t* id = a.out_ids + (size_t)b * a.k_final;
+    const int i = r - start;
+    if (on && i >= 0 && i < c) {
+      sc[i] = float_of_ord(ordk_of(v));
+      id[i] = (int64_t)gid_of(v);
+    }
+    for (int e = max(c, 0) + lane; e < a.k_final; e += 64) {
+      sc[e] = 0.f;
+      id[e] = -1;
+    }
+    if (a.out_counts && lane == 0) a.out_counts[b] = c;
+    return;
+  }
+  uint64_t* out = a.keys_out + (size_t)b * a.K;
+  if (on && r < cnt) out[r] = v;
+  for (int e = cnt + lane; e < a.K; e += 64) out[e] = 0ull;
+  if (lane == 0 && a.max_out) a.max_out[b] = a.drop ? gmax : 0ull;
+}
+
 __device__ __forceinline__ void sq_emit_any(const SqArgs& a, int b, const uint64_t* cb, int C, uint64_t gmax) {
-  if (C <= 64) sq_emit<1>(a, b, cb, C, gmax);
+  if (C <= 64 && (a.mopt & 2)) sq_emit_rank(a, b, cb, C, gmax);
+  else if (C <= 64) sq_emit<1>(a, b, cb, C, gmax);
   else if (C <= 128) sq_emit<2>(a, b, cb, C, gmax);
   else sq_emit<4>(a, b, cb, C, gmax);  // C <= kSqCand
 }
@@ -361,11 +400,11 @@ __device__ __forceinline__ float sq_margin(const SqArgs& a, const float* qrow) {
 // are in flight); the candidates are the list keys at or above it, plus every row of a
 // workgroup whose kSqM-th key reaches it that its list did not hold.  Returns the count (it
 // may exceed cap: the caller's slow path) and the bound.
-__device__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint32_t* ords, int K, const float* qrow,
+template <int NL>  // nwg <= 64·NL
+__device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint32_t* ords, int K, const float* qrow,
                               bool kth, uint64_t* cb, uint32_t cap, uint32_t* T_out) {
   const int lane = threadIdx.x & 63;
   const int nwg = a.nwg;
-  constexpr int NL = kSqMaxWg / 64;
   uint64_t ent[NL][kSqM];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
@@ -397,7 +436,11 @@ __device__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint3
 #pragma unroll
   for (int i = 0; i < NL; ++i)
 #pragma unroll
-    for (int j = 0; j < kSqM; ++j) base = wave_append(ordk_of(ent[i][j]) >= T, ent[i][j], cb, base, cap);
+    for (int j = 0; j < kSqM; ++j) {
+      const bool take = ordk_of(ent[i][j]) >= T;
+      if ((a.mopt & 1) && !__ballot(take)) break;  // each list is descending
+      base = wave_append(take, ent[i][j], cb, base, cap);
+    }
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     uint64_t ovm = __ballot(ordk_of(ent[i][kSqM - 1]) >= T);
@@ -438,7 +481,7 @@ __device__ __forceinline__ void sq_rescore(const SqArgs& a, uint64_t* keys, int 
 // Slow exact path (more candidates than the buffers hold: masses of equal scores): every
 // eligible row with order image >= Te and every present row >= Tp, rescored in batches of 256
 // into a running exact top-K (and running present maximum).
-__device__ void sq_slow(const SqArgs& a, int b, uint32_t Te, uint32_t Tp, const float* qs, uint64_t* eb,
+__device__ __forceinline__ void sq_slow(const SqArgs& a, int b, uint32_t Te, uint32_t Tp, const float* qs, uint64_t* eb,
                         uint64_t* pb, uint64_t* run, uint32_t* scan_sh, uint32_t* misc) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const uint32_t* oe = a.ords + (size_t)b * a.ords_ld;
@@ -486,17 +529,23 @@ __device__ void sq_slow(const SqArgs& a, int b, uint32_t Te, uint32_t Tp, const 
   if (w == 0) sq_emit_any(a, b, run, rc, gm);
 }
 
-// Merge: one workgroup per (side, query).
-__global__ __launch_bounds__(kSqThreads) void sq_merge_kernel(SqArgs a0, SqArgs a1) {
-  __shared__ __attribute__((aligned(16))) float qs[kRrMaxD];
-  __shared__ uint64_t cand[kSqCand + kSqPCand];
-  __shared__ uint64_t ptmp[kSqCand];
-  __shared__ uint64_t run[kSqMaxK];
-  __shared__ uint32_t scan_sh[kSelectThreads / 64];
-  __shared__ uint32_t misc[8];
-  const int side = (int)blockIdx.x >= a0.B ? 1 : 0;
-  const SqArgs& a = side ? a1 : a0;
-  const int b = (int)blockIdx.x - side * a0.B;
+struct SqMergeLds {
+  __attribute__((aligned(16))) float qs[kRrMaxD];
+  uint64_t cand[kSqCand + kSqPCand];
+  uint64_t ptmp[kSqCand];
+  uint64_t run[kSqMaxK];
+  uint32_t scan_sh[kSelectThreads / 64];
+  uint32_t misc[8];
+};
+
+// Merge of query b of one side (a: a kernel argument itself, so its fields stay scalar loads)
+__device__ __forceinline__ void sq_merge_row(const SqArgs& a, int b, SqMergeLds& L) {
+  float* qs = L.qs;
+  uint64_t* cand = L.cand;
+  uint64_t* ptmp = L.ptmp;
+  uint64_t* run = L.run;
+  uint32_t* scan_sh = L.scan_sh;
+  uint32_t* misc = L.misc;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int ldx = (int)a.ldx;
   const float* qrow = a.q_out + (size_t)b * ldx;
@@ -507,14 +556,19 @@ __global__ __launch_bounds__(kSqThreads) void sq_merge_kernel(SqArgs a0, SqArgs 
   for (int i = tid; i < ldx; i += kSqThreads) qs[i] = qrow[i];
   if (w == 0) {
     uint32_t T;
-    const uint32_t ce = sq_gather(a, a.wg_top + (size_t)b * a.nwg * kSqM, a.ords + (size_t)b * a.ords_ld, a.K, qrow,
-                                  true, cand, kSqCand, &T);
+    const uint64_t* tops = a.wg_top + (size_t)b * a.nwg * kSqM;
+    const uint32_t* ords = a.ords + (size_t)b * a.ords_ld;
+    const uint32_t ce = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, a.K, qrow, true, cand, kSqCand, &T)
+                                                      : sq_gather<8>(a, tops, ords, a.K, qrow, true, cand, kSqCand, &T);
     if (lane == 0) misc[0] = ce, misc[2] = T;
   } else if (w == 1) {
     uint32_t T = 0xFFFFFFFFu, cp = 0;
-    if (a.drop)
-      cp = sq_gather(a, a.wg_ptop + (size_t)b * a.nwg * kSqM, a.ords_p + (size_t)b * a.ords_ld, 1, qrow, false, ptmp,
-                     kSqPCand, &T);
+    if (a.drop) {
+      const uint64_t* tops = a.wg_ptop + (size_t)b * a.nwg * kSqM;
+      const uint32_t* ords = a.ords_p + (size_t)b * a.ords_ld;
+      cp = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, 1, qrow, false, ptmp, kSqPCand, &T)
+                                        : sq_gather<8>(a, tops, ords, 1, qrow, false, ptmp, kSqPCand, &T);
+    }
     if (lane == 0) misc[1] = cp, misc[3] = T;
   }
   __syncthreads();
@@ -539,6 +593,14 @@ __global__ __launch_bounds__(kSqThreads) void sq_merge_kernel(SqArgs a0, SqArgs 
     if (a.mtrace && lane == 0) a.mtrace[(size_t)b * 8 + 4] = ce | ((uint64_t)cp << 32);
   }
   stamp(3);
+}
+
+// Merge: one workgroup per (side, query); each side's body reads its own argument directly
+// (a reference selected between the two would copy both to the stack).
+__global__ __launch_bounds__(kSqThreads) void sq_merge_kernel(SqArgs a0, SqArgs a1) {
+  __shared__ SqMergeLds L;
+  if ((int)blockIdx.x < a0.B) sq_merge_row(a0, (int)blockIdx.x, L);
+  else sq_merge_row(a1, (int)blockIdx.x - a0.B, L);
 }
 
 template <int KS>

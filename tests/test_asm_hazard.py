@@ -51,3 +51,14 @@ def test_shipped_scan2_loads_are_retired_before_use():
     assert kernels >= 8, kernels          # every scan2 instantiation of the build
     assert sites >= 100, sites            # not a vacuous pass
     assert not bad, "\n".join(bad[:10])
+
+
+@needs_tools
+def test_small_batch_kernels_use_no_scratch_or_calls():
+    """The small-batch kernels (sq.hip) run on latency: no scratch traffic and no calls.  A
+    merge that selected a reference between its two by-value arguments, with its gather left
+    as a real function, copied both arguments to a 568-byte stack and called through it."""
+    fns = {n: ins for n, ins in H.functions(H.disassemble(H.LIB)).items() if "sq_" in n}
+    assert len(fns) >= 3, list(fns)
+    bad = {n[:80]: sum(("scratch_" in mn) or mn.startswith("s_swappc") for _, mn, _ in ins) for n, ins in fns.items()}
+    assert not any(bad.values()), bad

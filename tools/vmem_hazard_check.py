@@ -7,7 +7,7 @@ statement ends, so any instruction it placed between the load and that wait that
 copies or overwrites the destination register would see the old value (VERDICT r03 item 6;
 the same construct faulted in scan4's prologue in round 3).
 
-This tool extracts the gfx950 code object from libbrickrec.so (llvm-objcopy +
+This tool extracts the gfx950 code objects from libbrickrec.so (llvm-objcopy +
 clang-offload-bundler), disassembles it (llvm-objdump) and, for every
 `global_load_dword vN, ..., off` in the selected kernels, walks the control-flow graph from the
 next instruction — both ways at conditional branches — counting the vector-memory operations
@@ -35,15 +35,27 @@ LOADV = re.compile(r"^global_load_dword$")
 
 
 def disassemble(lib):
+    """Disassembly of every gfx950 code object in the library (one offload bundle per
+    translation unit, concatenated in .hip_fatbin)."""
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out = []
     with tempfile.TemporaryDirectory() as td:
-        fat, co = os.path.join(td, "fat.bin"), os.path.join(td, "dev.co")
+        fat = os.path.join(td, "fat.bin")
         subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fat}", lib, os.path.join(td, "x")],
                        check=True, capture_output=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True,
-                       capture_output=True)
-        return subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
-                              capture_output=True, text=True).stdout
+        data = open(fat, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+        for j, a in enumerate(starts):
+            part, co = os.path.join(td, f"b{j}.bin"), os.path.join(td, f"b{j}.co")
+            with open(part, "wb") as fh:
+                fh.write(data[a:starts[j + 1] if j + 1 < len(starts) else len(data)])
+            r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
+            if r.returncode != 0 or not os.path.getsize(co):
+                continue
+            out.append(subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
+                                      capture_output=True, text=True).stdout)
+    return "\n".join(out)
 
 
 def functions(text):
