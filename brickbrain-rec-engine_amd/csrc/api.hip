@@ -455,10 +455,12 @@ static int make_planes(bb_index* x, DevBuf& rows, DevBuf& planes, int ld) {
   return BB_OK;
 }
 
-// f32 index: the one-product bf16 copy + error statistics for the exact re-rank path (the
-// approximate bf16 MFMA scan, then the f32 rescoring of the candidates within its bound).
-// stat_off: 0 = item rows, 4 = CF factors.  Widths the bf16 scan or the re-rank cannot take
-// leave the copy unset (those searches run the split-precision scan instead).
+// f32 index: the one-product f16 copy + error statistics for the exact re-rank path (the
+// approximate f16 MFMA scan, then the f32 rescoring of the candidates within its bound; f16
+// keeps 11 significant bits to bf16's 8, so the bound and the candidate windows are ~1/8 as
+// wide: at configs[1] ~55 rescored rows per query for K = 51 instead of ~92).  stat_off: 0 =
+// item rows, 4 = CF factors.  Widths the 16-bit scan or the re-rank cannot take leave the
+// copy unset (those searches run the split-precision scan instead).
 static int make_rr(bb_index* x, DevBuf& rows, DevBuf& bf, int ld, int& ld_b, int stat_off) {
   ld_b = (int)round_up(ld, 64);
   if (x->dtype != F32 || ld > kRrMaxD || !gemm_uses_scan(BF16, kTileRows, ld_b)) {
@@ -1062,8 +1064,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       pa.Dpad = x->Dpad;
       pa.out = x->qn.p;
       pa.out_dtype = s3_c ? SPLIT3 : x->dtype;
-      if (rr_c) {  // bf16 operand + f32 row + bound
-        pa.out_dtype = BF16;
+      if (rr_c) {  // f16 operand + f32 row + bound
+        pa.out_dtype = F16;
         pa.Dpad = x->Dpad_b;
         pa.out_f32 = (float*)x->qf32.p;
         pa.Dpad_f = x->Dpad;
@@ -1092,7 +1094,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       pa.out = x->qcf.p;
       pa.out_dtype = s3_f ? SPLIT3 : x->dtype;
       if (rr_f) {
-        pa.out_dtype = BF16;
+        pa.out_dtype = F16;
         pa.Dpad = x->Rpad_b;
         pa.out_f32 = (float*)x->qcf32.p;
         pa.Dpad_f = x->Rpad;
@@ -1228,8 +1230,9 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         DevBuf& planes = cf_side ? x->cf3 : x->items3;
         const bool rr_side = cf_side ? rr_f : rr_c;
         if (rr_side) {
-          // approximate scan: bf16 queries x the one-product bf16 item copy
+          // approximate scan: f16 queries x the one-product f16 item copy
           const int64_t w = cf_side ? x->Rpad_b : x->Dpad_b;
+          ga.f16 = 1;
           ga.X = (const char*)(cf_side ? x->cf_bf.p : x->items_bf.p) + (size_t)c0 * w * 2;
           ga.ldx = ga.ldq = w;
           ga.Kpad = (int)w;

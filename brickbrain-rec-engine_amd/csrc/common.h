@@ -41,17 +41,40 @@ __device__ __forceinline__ uint16_t to_bf16(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// round-to-nearest-even f32 -> f16, saturating to ±65504 (the re-rank copy of an f32 index
+// and its query operands: every bound is computed from the rounded values, so a saturated
+// element only widens it; NaN kept NaN)
+__device__ __forceinline__ uint16_t to_f16(float f) {
+  const float c = f == f ? fminf(fmaxf(f, -65504.f), 65504.f) : f;
+  return __builtin_bit_cast(uint16_t, (_Float16)c);
+}
+__device__ __forceinline__ float f16_val(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+
+// γ per unit of row width: the f32 accumulation error of the approximate scans' 32x32x16
+// MFMA chains, as a fraction of Σ|x̃_j q̃_j| <= Ñ_x·‖q̃‖.  Each MFMA adds 16 exact products to
+// its accumulator; whatever the matrix core's order, rounding or truncation, each of those 17
+// values is off by at most 2^-23 of the largest partial sum, over width/16 chained MFMAs:
+// 17·(width/16)·2^-23 = (17/8)·width·2^-24.
+constexpr double kRrGamma = 17.0 / 8.0 * 0x1p-24;
+
 // ---- tiling constants ---------------------------------------------------------------------
 constexpr int kTileRows = 128;     // item / query rows are padded to this multiple
 constexpr int kSelectThreads = 256;
 constexpr int kSelectStageMax = 32768;  // score row staged in LDS when n_cols <= this
 constexpr int kMaxKInt = 512;      // per-side internal list length limit (k_side + 1)
 
-enum Dtype : int { F32 = 0, BF16 = 1, F64 = 2, SPLIT3 = 3 /* prep output: bf16 planes as the scan3 q3f image */ };
+enum Dtype : int {
+  F32 = 0,
+  BF16 = 1,
+  F64 = 2,
+  SPLIT3 = 3,  // prep output: bf16 planes as the scan3 q3f image
+  F16 = 4      // prep output: the f16 operand of the re-rank scans (never an index dtype)
+};
 
 struct GemmArgs {
   const void* Q;      // [Mpad][ldq]   queries (normalised), dtype of the index
   const void* X;      // [Npad][ldx]   item rows of the slab (row 0 = slab start)
+  int32_t f16;        // 16-bit operands are f16: the re-rank copy of an f32 index (kScanF16 scans)
   float* S;           // [Mpad][lds]   scores out
   int64_t ldq, ldx, lds;
   int32_t Mpad;       // multiple of the query block tile
@@ -139,6 +162,7 @@ constexpr int kScanStream = 512;  // scan ABL bit: streaming top-K epilogue
 constexpr int kScanS16 = 4096;    // scan ABL bit: int16 score image (GemmArgs.s_h)
 constexpr int kScanList = 8192;   // scan ABL bit: bounded candidate lists (GemmArgs.lists)
 constexpr int kScanPilot = 16384; // scan ABL bit: streaming pilot, top-m half-tile maxima (GemmArgs.pilot_top)
+constexpr int kScanF16 = 32768;   // scan ABL bit: f16 operands (the re-rank copy of an f32 index), not bf16
 
 // Quantum h of the int16 score image of one query and the widened bound of its decoded
 // scores.  |approximate score| <= |q̃|·Ñ_x·(1+γ) <= 16384·h, so no code saturates; the

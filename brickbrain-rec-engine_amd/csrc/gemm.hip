@@ -58,13 +58,19 @@ static void launch_scan_t(const GemmArgs& a, hipStream_t s) {
   // one workgroup per CU (LDS + VGPR budget): ~256 workgroups, chunks balanced to ±1 tile
   const int n_chunks = scan_n_chunks(a.Mpad, tiles);
   if constexpr (sizeof(T) == 2 && KU <= kRrMaxD / 8) {
-    if (a.lists) {  // exact re-rank path: bounded candidate lists
-      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanList>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
-                         n_chunks, tiles);
+    // the exact re-rank path: the f16 copy of an f32 index (launch_gemm checked a.f16)
+    if (a.lists) {  // bounded candidate lists
+      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanList | kScanF16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64),
+                         0, s, a, n_chunks, tiles);
       return;
     }
-    if (a.s_h && !a.cand) {  // exact re-rank path: int16 score image
-      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanS16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
+    if (a.s_h && !a.cand) {  // int16 score image
+      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanS16 | kScanF16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64),
+                         0, s, a, n_chunks, tiles);
+      return;
+    }
+    if (a.f16) {  // f32 score slab
+      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanF16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
                          n_chunks, tiles);
       return;
     }
@@ -139,7 +145,13 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   const int bm = gemm_tile_m(dtype), bn = gemm_tile_n(dtype), bk = gemm_tile_k(dtype);
   if (a.Mpad % bm || a.Ncols % bn || a.Kpad % bk || a.Mpad <= 0 || a.Ncols <= 0 || (a.slab_start & 31))
     return hipErrorInvalidValue;
-  // the fused re-rank prologue lives in scan2 (bf16, query chunks of <= 128 rows) only
+  // f16 operands (the re-rank copy): 16-bit scans of rows up to kRrMaxD, no streaming; the
+  // int16 image and the lists exist on that copy only
+  if ((a.f16 && (dtype != BF16 || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.Kpad > kRrMaxD || a.cand ||
+                 a.pilot_top)) ||
+      (!a.f16 && (a.s_h || a.lists || a.q_istats)))
+    return hipErrorInvalidValue;
+  // the fused re-rank prologue lives in scan2 (16-bit, query chunks of <= 128 rows) only
   if (a.q_istats && !a.q_raw && (dtype != BF16 || scan4_used(BF16, a.Mpad) || !a.q_f32_out || !a.q_eps_out || a.cand))
     return hipErrorInvalidValue;
   // the raw-query prologue: scan2 (bf16) with the list epilogue, raw f32 rows (d % 4 == 0)

@@ -20,6 +20,8 @@ __device__ __forceinline__ double load_elem_d(const void* p, int dtype, size_t i
 __device__ __forceinline__ void store_elem(void* p, int dtype, size_t i, float v) {
   if (dtype == BF16)
     ((uint16_t*)p)[i] = to_bf16(v);
+  else if (dtype == F16)
+    ((uint16_t*)p)[i] = to_f16(v);
   else
     ((float*)p)[i] = v;
 }
@@ -117,9 +119,10 @@ hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t
 }
 
 // ---------------------------------------------------------------------------------------
-// Re-rank operands of an f32 index: the one-product bf16 copy of every row (RNE) for the
-// approximate MFMA scan, and the statistics that bound its error (prep_kernel turns them
-// into the per-query ε): max over rows of ||x̃−x||, ||x||, ||x̃|| (f64 sums, rounded up to
+// Re-rank operands of an f32 index: the one-product f16 copy of every row (RNE, saturating)
+// for the approximate MFMA scan — 11 significant bits, so its error, and every bound and
+// candidate window built on it, is 1/8 of a bf16 copy's — and the statistics that bound that
+// error (prep_kernel turns them into the per-query ε): max over rows of ||x̃−x||, ||x||, ||x̃|| (f64 sums, rounded up to
 // f32, merged by integer atomicMax — non-negative floats order like their bit patterns).
 // One wave per row.
 // ---------------------------------------------------------------------------------------
@@ -131,8 +134,8 @@ __global__ __launch_bounds__(256) void rr_prepare_kernel(const float* src, int64
   double e2 = 0.0, n2 = 0.0, b2 = 0.0;
   for (int64_t i = lane; i < ld_b; i += 64) {
     const float v = i < ld_f ? src[row * ld_f + i] : 0.f;
-    const uint16_t hb = to_bf16(v);
-    const float bv = __builtin_bit_cast(float, (uint32_t)hb << 16);
+    const uint16_t hb = to_f16(v);
+    const float bv = f16_val(hb);
     dst[row * ld_b + i] = hb;
     const double dv = (double)v, db = (double)bv;
     e2 += (dv - db) * (dv - db);
@@ -182,27 +185,27 @@ __device__ __forceinline__ void store_q(const PrepArgs& a, int row, int i, float
     o[2 * plane] = l;
   } else if (a.q_perm) {  // bf16 operand in the scan's lane order
     const size_t o = a.q_perm == 2 ? scan2_q_offset(row, i >> 3, a.Dpad >> 4) : scan4_q_offset(row, i >> 3, a.Dpad >> 4);
-    ((uint16_t*)a.out)[o * 8 + (i & 7)] = to_bf16(v);
+    ((uint16_t*)a.out)[o * 8 + (i & 7)] = a.out_dtype == F16 ? to_f16(v) : to_bf16(v);
   } else {
     store_elem(a.out, a.out_dtype, (size_t)row * a.Dpad + i, v);
   }
 }
 
-// Re-rank outputs of one query row (PrepArgs.out_f32): the f32 element beside the bf16
+// Re-rank outputs of one query row (PrepArgs.out_f32): the f32 element beside the f16
 // operand, and ε = E_x·|q̃| + N_x·|q̃−q| + γ·Ñ_x·|q̃| — Cauchy-Schwarz on
-// Σ(x̃−x)q̃ + Σx(q̃−q), plus γ = 2·Dpad·2^-24 for the MFMA's f32 accumulation of Σx̃q̃.
+// Σ(x̃−x)q̃ + Σx(q̃−q), plus γ = kRrGamma·Dpad for the MFMA f32 accumulation of Σx̃q̃.
 struct RrAcc {
   double e2 = 0.0, b2 = 0.0;
   __device__ __forceinline__ void add(const PrepArgs& a, int row, int i, float v) {
     if (i < a.Dpad_f) a.out_f32[(size_t)row * a.Dpad_f + i] = v;
-    const double bv = (double)__builtin_bit_cast(float, (uint32_t)to_bf16(v) << 16);
+    const double bv = (double)f16_val(to_f16(v));
     e2 += ((double)v - bv) * ((double)v - bv);
     b2 += bv * bv;
   }
   __device__ __forceinline__ void finish(const PrepArgs& a, int row, int lane) {
     const double e = sqrt(wave_sum(e2)), b = sqrt(wave_sum(b2));
     if (lane == 0) {
-      const double gam = 2.0 * (double)a.Dpad * 0x1p-24;
+      const double gam = kRrGamma * (double)a.Dpad;
       const double eps = (double)a.istats[0] * b + (double)a.istats[1] * e + gam * (double)a.istats[2] * b;
       if (a.h_out) {  // int16 score image: its quantum, and ε widened to cover the codes
         rr_quantum(eps * (1.0 + 0x1p-20), b, (double)a.istats[2], a.eps_out[row], a.h_out[row]);

@@ -31,7 +31,26 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(std::make_integer_sequence<int, N>{}, f);
 }
 
-// Exact re-rank prologue (bf16 operand from raw f32 rows, GemmArgs.q_f32_out): lane half h
+// Two f32 -> one dword of the 16-bit operand (element a low): bf16 (v_cvt_pk_bf16_f32, RNE)
+// or, for the f16 re-rank copy (kScanF16), f16 (RNE, saturating: to_f16)
+template <bool F16>
+__device__ __forceinline__ uint32_t pack16(float a, float b) {
+  if constexpr (F16) {
+    return (uint32_t)to_f16(a) | ((uint32_t)to_f16(b) << 16);
+  } else {
+    typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+    const bf2v v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+  }
+}
+// element c (0: low half) of a packed dword, as f32
+template <bool F16>
+__device__ __forceinline__ float unpack16(uint32_t w, int c) {
+  if constexpr (F16) return f16_val((uint16_t)(c ? w >> 16 : w & 0xFFFFu));
+  else return __uint_as_float(c ? (w & 0xFFFF0000u) : (w << 16));
+}
+
+// Exact re-rank prologue (16-bit operand from raw f32 rows, GemmArgs.q_f32_out): lane half h
 // of query row q holds elements (2u + h)·8 .. +8 of the row.  Normalised in f64 as prep_kernel
 // (sklearn normalize); rounded to bf16 (v_cvt_pk_bf16_f32, RNE).
 // With rr_write (the workgroups of item chunk 0) the f32 row and ε go out as well:
@@ -39,9 +58,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 // scaled by (1 + 2^-10) to cover their rounding (<= 193 terms of 2^-24 each).
 // Source: raw rows q_src [M][q_src_ld], or (q_ids) the stored f32 item rows of the liked
 // sets, q_items_base [n][q_src_ld] (already normalised; an unknown id gives a zero row).
-template <int U>
+template <int U, bool F16>
 __device__ __forceinline__ void scan2_rr_prologue(const GemmArgs& a, int q, int h, bool rr_write, uint4 (&qf)[U]) {
-  typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
   bool ok = true;
   const float* row;
   if (a.q_ids) {
@@ -96,10 +114,7 @@ __device__ __forceinline__ void scan2_rr_prologue(const GemmArgs& a, int q, int 
     float4 p = kTwoPass ? load(u, 0) : x[2 * u], r = kTwoPass ? load(u, 1) : x[2 * u + 1];
     p = make_float4(scl(p.x), scl(p.y), scl(p.z), scl(p.w));
     r = make_float4(scl(r.x), scl(r.y), scl(r.z), scl(r.w));
-    const bf2v b0 = {(__bf16)p.x, (__bf16)p.y}, b1 = {(__bf16)p.z, (__bf16)p.w};
-    const bf2v b2v = {(__bf16)r.x, (__bf16)r.y}, b3 = {(__bf16)r.z, (__bf16)r.w};
-    qf[u] = make_uint4(__builtin_bit_cast(uint32_t, b0), __builtin_bit_cast(uint32_t, b1),
-                       __builtin_bit_cast(uint32_t, b2v), __builtin_bit_cast(uint32_t, b3));
+    qf[u] = make_uint4(pack16<F16>(p.x, p.y), pack16<F16>(p.z, p.w), pack16<F16>(r.x, r.y), pack16<F16>(r.z, r.w));
     if (rr_write) {
       const uint32_t w[4] = {qf[u].x, qf[u].y, qf[u].z, qf[u].w};
 #pragma unroll
@@ -110,9 +125,8 @@ __device__ __forceinline__ void scan2_rr_prologue(const GemmArgs& a, int q, int 
         const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const uint32_t ww = w[2 * s + (c >> 1)];
-          const float bv = __uint_as_float((c & 1) ? (ww & 0xFFFF0000u) : (ww << 16));
-          const float e = vv[c] - bv;  // exact (bv is vv[c] rounded to 8 significant bits)
+          const float bv = unpack16<F16>(w[2 * s + (c >> 1)], c & 1);
+          const float e = vv[c] - bv;  // exact (bv is vv[c] rounded to 8 or 11 significant bits)
           e2 = fmaf(e, e, e2);
           b2 = fmaf(bv, bv, b2);
         }
@@ -125,7 +139,7 @@ __device__ __forceinline__ void scan2_rr_prologue(const GemmArgs& a, int q, int 
   if (h == 0) {
     const double sc = 1.0 + 0x1p-10;
     const double e = sqrt((double)e2 * sc), b = sqrt((double)b2 * sc);
-    const double gam = 2.0 * (double)a.Kpad * 0x1p-24;
+    const double gam = kRrGamma * (double)a.Kpad;
     const double eps = (double)a.q_istats[0] * b + (double)a.q_istats[1] * e + gam * (double)a.q_istats[2] * b;
     if (a.q_h_out)
       rr_quantum(eps * (1.0 + 0x1p-20), b, (double)a.q_istats[2], a.q_eps_out[q], a.q_h_out[q]);
@@ -146,9 +160,8 @@ __device__ __forceinline__ void scan2_rr_prologue(const GemmArgs& a, int q, int 
 //   ε' = (ε·(1+2^-20) + 1.01·h + Q·(N_x·(2^-23 + 2^-40) + 2^-20))·(1+2^-20)
 // where the Q term covers the exact score's own roundings (the normalised f32 row, the f64
 // sum rounded to f32) against x·q/‖q‖, scaled to raw units.
-template <int U>
+template <int U, bool F16>
 __device__ __forceinline__ float scan2_raw_prologue(const GemmArgs& a, int q, int h, bool write, uint4 (&qf)[U]) {
-  typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
   const float* row = (const float*)a.q_src + (size_t)q * a.q_src_ld;
   const int d = a.q_d;
   float n2 = 0.f, e2 = 0.f, b2 = 0.f;
@@ -165,18 +178,15 @@ __device__ __forceinline__ float scan2_raw_prologue(const GemmArgs& a, int q, in
       n2 = fmaf(v[s].z, v[s].z, n2);
       n2 = fmaf(v[s].w, v[s].w, n2);
     }
-    const bf2v b0 = {(__bf16)v[0].x, (__bf16)v[0].y}, b1 = {(__bf16)v[0].z, (__bf16)v[0].w};
-    const bf2v b2v = {(__bf16)v[1].x, (__bf16)v[1].y}, b3 = {(__bf16)v[1].z, (__bf16)v[1].w};
-    qf[u] = make_uint4(__builtin_bit_cast(uint32_t, b0), __builtin_bit_cast(uint32_t, b1),
-                       __builtin_bit_cast(uint32_t, b2v), __builtin_bit_cast(uint32_t, b3));
+    qf[u] = make_uint4(pack16<F16>(v[0].x, v[0].y), pack16<F16>(v[0].z, v[0].w), pack16<F16>(v[1].x, v[1].y),
+                       pack16<F16>(v[1].z, v[1].w));
     if (write) {  // (wave-uniform: the workgroups of item chunk 0)
       const uint32_t w[4] = {qf[u].x, qf[u].y, qf[u].z, qf[u].w};
       const float vv[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const uint32_t ww = w[c >> 1];
-        const float bv = __uint_as_float((c & 1) ? (ww & 0xFFFF0000u) : (ww << 16));
-        const float e = vv[c] - bv;  // exact (bv is vv[c] rounded to 8 significant bits)
+        const float bv = unpack16<F16>(w[c >> 1], c & 1);
+        const float e = vv[c] - bv;  // exact (bv is vv[c] rounded to 8 or 11 significant bits)
         e2 = fmaf(e, e, e2);
         b2 = fmaf(bv, bv, b2);
       }
@@ -192,7 +202,7 @@ __device__ __forceinline__ float scan2_raw_prologue(const GemmArgs& a, int q, in
       const double sc = 1.0 + 0x1p-10;
       const double e = sqrt((double)e2 * sc), b = sqrt((double)b2 * sc);
       const double ex = (double)a.q_istats[0], nx = (double)a.q_istats[1], nxb = (double)a.q_istats[2];
-      const double gam = 2.0 * (double)a.Kpad * 0x1p-24;
+      const double gam = kRrGamma * (double)a.Kpad;
       const double eps = ex * b + nx * e + gam * nxb * b;
       const double ep = (eps * (1.0 + 0x1p-20) + 1.01 * (double)hq + Q * (nx * (0x1p-23 + 0x1p-40) + 0x1p-20)) *
                         (1.0 + 0x1p-20);
@@ -205,7 +215,7 @@ __device__ __forceinline__ float scan2_raw_prologue(const GemmArgs& a, int q, in
 
 // Query operand: 16-B chunk (2u + h) of this lane's query row into qf[u].  Returns the list
 // epilogue's code quantum of the raw-query prologue (0 otherwise: the epilogue reads s_h).
-template <typename T, int KU>
+template <typename T, int KU, bool F16 = false>
 __device__ __forceinline__ float scan2_load_queries(const GemmArgs& a, int q, int h, uint4 (&qf)[KU / 2],
                                                     bool rr_write = false) {
   constexpr int U = KU / 2;
@@ -215,9 +225,9 @@ __device__ __forceinline__ float scan2_load_queries(const GemmArgs& a, int q, in
     return 0.f;
   }
   if constexpr (sizeof(T) == 2 && KU <= kRrMaxD / 8) {
-    if (a.q_raw) return scan2_raw_prologue<U>(a, q, h, rr_write, qf);
+    if (a.q_raw) return scan2_raw_prologue<U, F16>(a, q, h, rr_write, qf);
     if (a.q_istats) {  // exact re-rank operands (GemmArgs.q_f32_out)
-      scan2_rr_prologue<U>(a, q, h, rr_write, qf);
+      scan2_rr_prologue<U, F16>(a, q, h, rr_write, qf);
       return 0.f;
     }
   }
@@ -425,8 +435,11 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   const int q = group * kScanWaves * 32 + wave * 32 + r;
   if (tile_lo >= tile_hi) return;  // uniform per workgroup
 
+  // f16 operands: the re-rank copy of an f32 index (kScanF16); bf16 otherwise
+  constexpr bool F16 = (ABL & kScanF16) != 0;
+  static_assert(!F16 || sizeof(T) == 2, "f16 operands are 16-bit");
   uint4 qf[U];
-  const float hq_raw = scan2_load_queries<T, KU>(a, q, h, qf, chunk == 0 && a.q_istats != nullptr);
+  const float hq_raw = scan2_load_queries<T, KU, F16>(a, q, h, qf, chunk == 0 && a.q_istats != nullptr);
   float qa[sizeof(T) == 4 ? 4 * U : 1];  // f32: the operand as 4U scalars, pinned to AGPRs
   if constexpr (sizeof(T) == 4) {
 #pragma unroll
@@ -574,10 +587,17 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
         }
       } else {
         const u32x4v fv = __builtin_bit_cast(u32x4v, fa);
-        if constexpr (u == 0)
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[u]));
-        else
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[u]));
+        if constexpr (F16) {
+          if constexpr (u == 0)
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[u]));
+          else
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[u]));
+        } else {
+          if constexpr (u == 0)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[u]));
+          else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[u]));
+        }
       }
       if constexpr (u > 0) asm volatile("" ::"v"(__builtin_bit_cast(u32x4v, fq[(u + 3) % 4])));
       // ---- list epilogue (kScanList): eligibility, 16 half-pair slices (codes, keys, top-5

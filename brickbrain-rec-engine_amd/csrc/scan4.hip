@@ -30,12 +30,19 @@ static void launch_t(const GemmArgs& a, hipStream_t s) {
   const int n_chunks = scan4_n_chunks(a.Mpad, tiles);
   const int blocks = a.Mpad / kScan4Queries * n_chunks;
   if constexpr (KU <= kRrMaxD / 8) {
-    if (a.lists) {  // exact re-rank path: bounded candidate lists
-      hipLaunchKernelGGL((scan4_kernel<KU, kScanList>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+    // the exact re-rank path: the f16 copy of an f32 index
+    if (a.lists) {  // bounded candidate lists
+      hipLaunchKernelGGL((scan4_kernel<KU, kScanList | kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a,
+                         n_chunks, tiles);
       return;
     }
-    if (a.s_h && !a.cand) {  // exact re-rank path: int16 score image
-      hipLaunchKernelGGL((scan4_kernel<KU, kScanS16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+    if (a.s_h && !a.cand) {  // int16 score image
+      hipLaunchKernelGGL((scan4_kernel<KU, kScanS16 | kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a,
+                         n_chunks, tiles);
+      return;
+    }
+    if (a.f16) {  // f32 score slab
+      hipLaunchKernelGGL((scan4_kernel<KU, kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
       return;
     }
   }
@@ -54,12 +61,12 @@ static void launch_dual_t(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s)
   const int t0 = a0.Ncols / 32, t1 = a1.Ncols / 32;
   const int nc0 = scan4_n_chunks(a0.Mpad, t0), nc1 = scan4_n_chunks(a1.Mpad, t1);
   const int nb0 = a0.Mpad / kScan4Queries * nc0, nb1 = a1.Mpad / kScan4Queries * nc1;
-  if (a0.lists)  // bounded candidate lists on both sides
-    hipLaunchKernelGGL((scan4_dual_kernel<KU0, KU1, kScanList>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0, s, a0,
-                       a1, nc0, t0, nc1, t1, nb0);
+  if (a0.lists)  // bounded candidate lists on both sides (the f16 re-rank copies)
+    hipLaunchKernelGGL((scan4_dual_kernel<KU0, KU1, kScanList | kScanF16>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0,
+                       s, a0, a1, nc0, t0, nc1, t1, nb0);
   else
-    hipLaunchKernelGGL((scan4_dual_kernel<KU0, KU1, kScanS16>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0, s, a0,
-                       a1, nc0, t0, nc1, t1, nb0);
+    hipLaunchKernelGGL((scan4_dual_kernel<KU0, KU1, kScanS16 | kScanF16>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0,
+                       s, a0, a1, nc0, t0, nc1, t1, nb0);
 }
 template <int KU0>
 static bool launch_dual_k1(const GemmArgs& a0, const GemmArgs& a1, int ku1, hipStream_t s) {
@@ -74,7 +81,8 @@ bool scan4_dual_supported(int ku0, int ku1) {
 }
 hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
   const int ku0 = a0.Kpad * 2 / 16, ku1 = a1.Kpad * 2 / 16;
-  if (!scan4_dual_supported(ku0, ku1) || !a0.s_h || !a1.s_h || a0.cand || a1.cand || !scan4_used(BF16, a0.Mpad) ||
+  if (!scan4_dual_supported(ku0, ku1) || !a0.s_h || !a1.s_h || !a0.f16 || !a1.f16 || a0.cand || a1.cand ||
+      !scan4_used(BF16, a0.Mpad) ||
       !a0.lists != !a1.lists || (a0.lists && (a0.l_period <= 0 || a0.l_np <= 0 || a1.l_period <= 0 || a1.l_np <= 0)) ||
       a0.Mpad != a1.Mpad || a0.Ncols % 32 || a1.Ncols % 32 || (a0.slab_start & 31) || (a1.slab_start & 31) || a0.q_ids ||
       a0.q_src || a0.q_istats || a1.q_ids || a1.q_src || a1.q_istats)

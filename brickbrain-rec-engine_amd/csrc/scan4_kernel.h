@@ -145,6 +145,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   static_assert(ROWB <= kScanRowMax, "row too wide for the scan kernel");
   static_assert(KU % 8 == 0, "KU must split into whole 1 KiB pieces per wave");
   constexpr bool STREAM = (ABL & kScanStream) != 0;
+  constexpr bool F16 = (ABL & kScanF16) != 0;  // f16 operands: the re-rank copy of an f32 index
   // item tile ring, + (streaming) a 4-KiB register parking area per wave for the appends
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE_B + (STREAM ? kScanWaves * 4096 : 0)];
 
@@ -473,17 +474,31 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       const u32x4v fv = fq[st % 4];
       f32x16s& c = b ? accB : accA;
       if constexpr (st < NA) {
-        if constexpr (u == 0)
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[st]));
-        else
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[st]));
+        if constexpr (u == 0) {
+          if constexpr (F16)
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[st]));
+          else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[st]));
+        } else {
+          if constexpr (F16)
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[st]));
+          else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[st]));
+        }
       } else {
         // VGPR-resident query operand: the s_nop covers a VALU write (a copy the register
         // allocator may place) -> MFMA read hazard the compiler cannot see through asm
-        if constexpr (u == 0)
-          asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "v"(qv[st]));
-        else
-          asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "v"(qv[st]));
+        if constexpr (u == 0) {
+          if constexpr (F16)
+            asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "v"(qv[st]));
+          else
+            asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "v"(qv[st]));
+        } else {
+          if constexpr (F16)
+            asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "v"(qv[st]));
+          else
+            asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "v"(qv[st]));
+        }
       }
       if constexpr (st > 0) asm volatile("" ::"v"(fq[(st + 3) % 4]));
       // the other block's accumulator: its chain ended >= 2 MFMAs ago; the tie makes every
@@ -574,10 +589,17 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
         if constexpr (b == 0 && u + 2 < U) fq[(u + 2) % 4] = frag(u + 2);
         const u32x4v fv = fq[u % 4];
         f32x16s& c = b ? cB : cA;
-        if constexpr (u == 0)
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[b * U + u]));
-        else
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[b * U + u]));
+        if constexpr (u == 0) {
+          if constexpr (F16)
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[b * U + u]));
+          else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "a"(qv[b * U + u]));
+        } else {
+          if constexpr (F16)
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[b * U + u]));
+          else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[b * U + u]));
+        }
         if constexpr (b == 0 && u > 0) asm volatile("" ::"v"(fq[(u + 3) % 4]));
         if constexpr (st == 1 && epi) asm volatile("s_nop 15" : "+v"(pA), "+v"(pB));
         if constexpr (LIST) {

@@ -1,7 +1,7 @@
 // sq.h — small-batch exact search (sq.hip): the arguments shared by api.hip and the kernels.
 //
-// B <= kSqMaxB query rows of one side against an f32 index (that has its bf16 copy): ONE
-// approximate pass over the bf16 rows on the matrix cores (bf16 rows x bf16 hi + lo query
+// B <= kSqMaxB query rows of one side against an f32 index (that has its f16 copy): ONE
+// approximate pass over the f16 rows on the matrix cores (f16 rows x f16 hi + lo query
 // split, f32 accumulation) — every approximate score a within a proven δ of the exact score s (the f32 products summed in f64 in rescore_rows' fixed order, rounded to
 // f32) — leaves per workgroup and query its top kSqM approximate keys (and present keys for the
 // rank-0 drop) and every row's approximate order image; the merge (one workgroup per query and
@@ -21,7 +21,7 @@ constexpr int kSqCand = 256;    // eligible candidates per query the merge sorts
 constexpr int kSqPCand = 64;    // rank-0 candidates per query (beyond: the slow exact path)
 
 struct SqArgs {
-  const uint16_t* Xb;       // bf16 rows [n][ldb] (the index's round-to-nearest copy, zero padded)
+  const uint16_t* Xb;       // f16 rows [n][ldb] (the index's round-to-nearest copy, zero padded)
   int64_t ldb;
   const float* X;           // f32 rows [n][ldx], normalised, zero padded: the exact rescore
   int64_t ldx;
@@ -63,7 +63,7 @@ struct SqArgs {
   uint64_t* mtrace;         //   and merge phase stamps [B][8] of this side, or null
 };
 
-// rows per pass workgroup whose bf16 rows (ldb wide), B query rows (ldx wide) and order images
+// rows per pass workgroup whose f16 rows (ldb wide), B query rows (ldx wide) and order images
 // fit the LDS at once (a multiple of 16, <= kSqMaxRows)
 int sq_rows_cap(int64_t ldb, int B, int64_t ldx);
 

@@ -6,9 +6,9 @@
 // one liked set (:612-677).  For such batches the MFMA scan + per-lane lists + list select of
 // the large-batch path is mostly latency; here (sq.h):
 //
-//   pass   workgroup blk stages rows [blk·rpw, +rpw) of the bf16 copy into LDS by LDS-DMA
+//   pass   workgroup blk stages rows [blk·rpw, +rpw) of the f16 copy into LDS by LDS-DMA
 //          (the whole block in flight at once) and scores them on the matrix cores against the
-//          query rows split into bf16 hi + lo (16 queries per MFMA column block, f32
+//          query rows split into f16 hi + lo (16 queries per MFMA column block, f32
 //          accumulation): a = Σ x̃_j (h_j + l_j).  |a − s| <= δ (sq_margin) for the exact score s
 //          (E_x, N_x, Ñ_x = rr_stats).  Per query it leaves its top kSqM eligible (and present)
 //          approximate keys and every row's approximate order image.
@@ -33,7 +33,7 @@ constexpr int kSqThreads = 256;
 constexpr int kSqWaves = kSqThreads / 64;
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
-// 16 B of LDS as four u32 (bf16 pairs).  (Read as a float vector, __builtin_bit_cast of its
+// 16 B of LDS as four u32 (16-bit pairs).  (Read as a float vector, __builtin_bit_cast of its
 // .y/.z/.w elements compiled to a single ds_read_b32 whose .x stood in for all four on ROCm
 // 7.2 — wrong operands, not a fault.)
 __device__ __forceinline__ u4v lds_u4(const void* p, int c) {
@@ -113,7 +113,9 @@ __device__ __forceinline__ void sq_emit_rank(const SqArgs& a, int b, const uint6
   const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
   int r = 0;
   for (int j = 0; j < C; ++j) {  // uniform
-    const uint64_t y = ((uint64_t)__builtin_amdgcn_readlane(vhi, j) << 32) | __builtin_amdgcn_readlane(vlo, j);
+    // (readlane returns int: each half goes through uint32_t, or the low one sign-extends)
+    const uint64_t y = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, j) << 32) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vlo, j);
     r += y > v;
   }
   const bool on = lane < C;
@@ -173,22 +175,26 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return max(max(a, b), max(c, d));
 }
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-// eight f32 -> bf16 (round to nearest even) packed as the MFMA operand
-__device__ __forceinline__ u4v pack_bf16x8(const float (&v)[8]) {
-  u4v r;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// the query split of one 8-element k-group: hi = f16(v) and lo = f16(v − hi) (RNE,
+// saturating: to_f16), packed as the MFMA's B operands.  The merge recomputes both from the
+// f32 row for the bound (sq_margin), so nothing here is assumed about their accuracy.
+__device__ __forceinline__ void split_f16x8(const float (&v)[8], u4v& hi, u4v& lo) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = (uint32_t)to_bf16(v[2 * i]) | ((uint32_t)to_bf16(v[2 * i + 1]) << 16);
-  return r;
+  for (int i = 0; i < 4; ++i) {
+    const uint16_t h0 = to_f16(v[2 * i]), h1 = to_f16(v[2 * i + 1]);
+    hi[i] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+    lo[i] = (uint32_t)to_f16(v[2 * i] - f16_val(h0)) | ((uint32_t)to_f16(v[2 * i + 1] - f16_val(h1)) << 16);
+  }
 }
 
 // Approximate pass on the matrix cores.  The workgroup's rows are staged into LDS by LDS-DMA
 // (the whole block in flight at once, one wait) in a chunk-major image: 16-row chunks, and in
 // a chunk the 16-B column cc of row r at slot cc·16 + r — one 1-KiB LDS-DMA piece (64 slots) per
 // four columns, and the MFMA operand of a 32-wide k-step is one contiguous, conflict-free
-// 1-KiB wave read.  Each wave scores whole chunks: per k-step two v_mfma_f32_16x16x32_bf16 —
-// the bf16 rows (A: 16 rows x 32) against the query rows split into bf16 hi + lo (B: 32 x 16
-// queries, up to 16 per launch; q − hi − lo <= 2^-18·|q|), f32 accumulation.  KS = ldb / 32.
+// 1-KiB wave read.  Each wave scores whole chunks: per k-step two v_mfma_f32_16x16x32_f16 —
+// the f16 rows (A: 16 rows x 32) against the query rows split into f16 hi + lo (B: 32 x 16
+// queries, up to 16 per launch; |q − hi − lo| <= 2^-22·|q|), f32 accumulation.  KS = ldb / 32.
 template <int KS>
 __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sq_smem[];
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows' LDS-DMA has landed
   __syncthreads();
   stamp(2);
-  // the B operand: lane l holds query n = l & 15, k = 32·ks + 8·(l >> 4) + j, as bf16 hi + lo
+  // the B operand: lane l holds query n = l & 15, k = 32·ks + 8·(l >> 4) + j, as f16 hi + lo
   u4v qhi[KS], qlo[KS];
   {
     const int n = lane & 15;
@@ -271,14 +277,8 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
       const bool on = n < B && k0 < ldx;
       const f4v v0 = on ? lds_f4(qs + n * ldx, k0 >> 2) : f4v{0.f, 0.f, 0.f, 0.f};
       const f4v v1 = on ? lds_f4(qs + n * ldx, (k0 >> 2) + 1) : f4v{0.f, 0.f, 0.f, 0.f};
-      float h[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w}, l[8];
-      qhi[ks] = pack_bf16x8(h);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float hb = __uint_as_float((uint32_t)to_bf16(h[j]) << 16);
-        l[j] = h[j] - hb;  // exact (the f32 residual of the bf16 rounding)
-      }
-      qlo[ks] = pack_bf16x8(l);
+      const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      split_f16x8(v, qhi[ks], qlo[ks]);
     }
   }
   for (int c = w; c < nck; c += kSqWaves) {  // wave-uniform
@@ -289,10 +289,10 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
     f4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[ks]), __builtin_bit_cast(bf16x8, qhi[ks]),
-                                                    acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[ks]), __builtin_bit_cast(bf16x8, qlo[ks]),
-                                                    acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[ks]), __builtin_bit_cast(f16x8, qhi[ks]),
+                                                   acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[ks]), __builtin_bit_cast(f16x8, qlo[ks]),
+                                                   acc, 0, 0, 0);
     }
     const int n = lane & 15, rb = 16 * c + 4 * (lane >> 4);  // D: query n, rows rb .. rb + 3
     if (n < B) {
@@ -374,23 +374,40 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
 }
 
 // the re-rank margin 2δ (rr_margin) of a query row, every lane of the wave (qrow: the f32 row,
-// ldx wide):  δ = ‖q‖·(E_x + (γ + 2^-17)·Ñ_x + 2^-23·N_x) — Cauchy–Schwarz on Σ(x̃_j − x_j)q_j
-// (E_x), the hi + lo split residual |q − h − l| <= 2^-18·|q| against x̃ (2^-17·Ñ_x, with room),
-// the f32 accumulation of the 2·ldb exact bf16 products whatever the matrix core's order,
-// rounding or truncation (γ = 8·ldb·2^-24 >= (2·ldb)·2^-23 · Σ|h|+|l| / ‖q‖, with room), and
-// the f32 rounding of s (2^-23·N_x)
+// ldx wide), with h, l the pass's f16 split of q and r = q − h − l (recomputed here in f64):
+//   δ = E_x·‖q‖ + Ñ_x·‖r‖ + γ·Ñ_x·(‖h‖ + ‖l‖) + 2^-23·N_x·‖q‖
+// — Σ(x̃_j − x_j)q_j by Cauchy–Schwarz (E_x); Σ x̃_j r_j (the split's residual); the f32
+// accumulation of the 2·ldb exact f16 products, Σ|x̃_j|(|h_j| + |l_j|) <= Ñ_x(‖h‖ + ‖l‖), over
+// 2·ldb/32 chained MFMAs of 32 products + the accumulator each, every one of the 33 values
+// rounded or truncated by at most 2^-23 of the largest partial sum whatever the matrix core's
+// order (γ = 33·(2·ldb/32)·2^-23); and the f32 rounding of s (2^-23·N_x).  E_x, N_x, Ñ_x =
+// rr_stats of the side.
 __device__ __forceinline__ float sq_margin(const SqArgs& a, const float* qrow) {
   const int lane = threadIdx.x & 63, ldx = (int)a.ldx;
   float v[kQnC];
 #pragma unroll
   for (int c = 0; c < kQnC; ++c) v[c] = qrow[min(lane + 64 * c, ldx - 1)];
-  double ss = 0.0;
+  double qq = 0.0, rr = 0.0, hh = 0.0, ll = 0.0;
 #pragma unroll
-  for (int c = 0; c < kQnC; ++c) ss = fma(lane + 64 * c < ldx ? (double)v[c] : 0.0, (double)v[c], ss);
-  ss = qn_wave_sum(ss);
-  const double qn = sqrt(ss) * (1.0 + 0x1p-40);
-  const double gam = (double)a.ldb * 0x1p-21 + 0x1p-17;
-  const double d = qn * ((double)a.stats[0] + gam * (double)a.stats[2] + 0x1p-23 * (double)a.stats[1]);
+  for (int c = 0; c < kQnC; ++c) {
+    const float x = lane + 64 * c < ldx ? v[c] : 0.f;
+    const double h = (double)f16_val(to_f16(x));
+    const double l = (double)f16_val(to_f16(x - (float)h));
+    const double r = (double)x - h - l;
+    qq = fma((double)x, (double)x, qq);
+    rr = fma(r, r, rr);
+    hh = fma(h, h, hh);
+    ll = fma(l, l, ll);
+  }
+  qq = qn_wave_sum(qq);
+  rr = qn_wave_sum(rr);
+  hh = qn_wave_sum(hh);
+  ll = qn_wave_sum(ll);
+  const double up = 1.0 + 0x1p-40;
+  const double qn = sqrt(qq) * up, rn = sqrt(rr) * up, sn = (sqrt(hh) + sqrt(ll)) * up;
+  const double gam = 33.0 * (2.0 * (double)a.ldb / 32.0) * 0x1p-23;
+  const double ex = (double)a.stats[0], nx = (double)a.stats[1], nxb = (double)a.stats[2];
+  const double d = ex * qn + nxb * rn + gam * nxb * sn + 0x1p-23 * nx * qn;
   return rr_margin(__double2float_ru(d * (1.0 + 0x1p-20)));
 }
 
