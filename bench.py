@@ -23,8 +23,8 @@ candidate keys, bb_finalize merge) fix the total items, so more GPUs means small
 Roofline (dominant kernel = the scan launches of a step, HIP events on the library's launch
 stream; see roofline()): the binding side follows SURVEY.md §8(d), max(issued MFMA flops /
 MFMA peak, algorithmic bytes / HBM peak).  The f32 index runs the exact re-rank path (a
-one-product bf16 MFMA scan, then rerank_kernel rescores the candidates within its proven
-error bound from the f32 rows), so at configs[1] the algorithmic model binds on HBM (39.2 MB
+one-product f16 MFMA scan over the index's f16 copy, then the list select rescores the
+candidates within its proven error bound from the f32 rows), so at configs[1] the algorithmic model binds on HBM (39.2 MB
 of f32 rows vs 4.96 GFLOP).  `f32_equivalent` prices the algorithmic flops against the f32
 MFMA peak (157.3 TF).
 
@@ -46,14 +46,14 @@ sys.path.insert(0, os.path.join(ROOT, "brickbrain-rec-engine_amd"))
 
 N_ITEMS, DIM, BATCH, TOPK = 25216, 384, 256, 50
 HBM_PEAK_GBS = 8000.0
-BF16_DENSE_TF = 2500.0   # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md), no sparsity
+BF16_DENSE_TF = 2500.0   # MI355X dense bf16 / f16 MFMA peak (MI355X_MICROARCH.md), no sparsity
 F32_DENSE_TF = 157.3
 
 
 def scan_kernel_info(dtype, width, batch):
     """(kernel, MFMA flops executed per algorithmic flop) of the scan that runs for an index
     of this dtype and padded width on a one-slab search.  An f32 index runs the exact
-    re-rank path: a one-product bf16 MFMA scan (scan2 for up to 256 queries, scan4 above)
+    re-rank path: a one-product f16 MFMA scan (scan2 for up to 256 queries, scan4 above)
     gives approximate scores within a proven bound and keeps bounded per-lane candidate lists,
     and select_list_kernel rescores the candidates within the bound from the f32 rows
     (BB_AB=1 BB_NO_RR forces the older split-precision scan3, six bf16 products per fp32
@@ -67,7 +67,7 @@ def scan_kernel_info(dtype, width, batch):
     if dtype == "f32" and ab and os.environ.get("BB_NO_RR"):
         return "scan2_kernel<float> (fp32 MFMA)", 1.0
     if dtype == "f32":
-        return (f"{kern}<uint16_t,{width * 2 // 16},list> (one-product bf16 approximate scan, bounded per-lane "
+        return (f"{kern}<uint16_t,{width * 2 // 16},list|f16> (one-product f16 approximate scan, bounded per-lane "
                 f"candidate lists in the epilogue, no score image; exact f32 re-rank of the candidates in "
                 f"select_list_kernel)"), 1.0
     return f"{kern}<uint16_t,{width * 2 // 16}> (bf16 MFMA)", 1.0
@@ -82,7 +82,7 @@ def roofline(flops_alg, bytes_alg, kernel_us, dtype, kname, mfma_per_flop, traff
     t = kernel_us * 1e-6
     alg_tf = flops_alg / t / 1e12
     issued = alg_tf * mfma_per_flop
-    peak_tf = BF16_DENSE_TF if (dtype == "bf16" or mfma_per_flop > 1 or "bf16" in kname) else F32_DENSE_TF
+    peak_tf = BF16_DENSE_TF if (dtype == "bf16" or mfma_per_flop > 1 or "bf16" in kname or "f16" in kname) else F32_DENSE_TF
     gbs = bytes_alg / t / 1e9
     t_mfma = flops_alg * mfma_per_flop / (peak_tf * 1e12)
     t_hbm = bytes_alg / (HBM_PEAK_GBS * 1e9)
@@ -108,7 +108,7 @@ def roofline(flops_alg, bytes_alg, kernel_us, dtype, kname, mfma_per_flop, traff
 def family_kernels(workload, dtype, B, scan_name):
     """Kernel behind each profiling family of bb_get_profile (HIP events on the launch stream)."""
     if workload == "c2" and dtype == "f32" and B <= 16:
-        return {"gemm": "sq_scan_kernel (one exact f32/f64 pass, small batch)", "select": "sq_merge_kernel"}
+        return {"gemm": "sq_scan_kernel (approximate f16 MFMA pass, small batch)", "select": "sq_merge_kernel"}
     if workload == "c3":
         return {"prep": "prep2_kernel", "gemm": scan_name, "select": "select_list_dual_kernel",
                 "finalize": "finalize1_kernel"}
@@ -671,7 +671,7 @@ def main():
         kname, mpf = scan_kernel_info(args.dtype, DIM, B)
         ab = os.environ.get("BB_AB")
         if args.dtype == "f32" and not (ab and os.environ.get("BB_NO_RR")) and not (ab and os.environ.get("BB_DUAL") == "0"):
-            kname = ("scan4_dual_kernel<48,8,list> (content d=384 + CF r=50 one-product bf16 scans in one launch, "
+            kname = ("scan4_dual_kernel<48,8,list|f16> (content d=384 + CF r=50 one-product f16 scans in one launch, "
                      "bounded per-lane candidate lists; exact f32 re-rank of the candidates in the list select)")
     else:
         flops = 2.0 * B * N_ITEMS * DIM

@@ -740,21 +740,17 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   const int sq_sel = x->sq_opt >= 0 ? x->sq_opt : sq_env;
   const bool sq_sides = (!need_content || (x->items_bf.p && x->Dpad <= kRrMaxD && x->d <= kRrMaxD && x->Dpad_b <= 512)) &&
                         (!need_cf || (x->cf_bf.p && x->Rpad <= kRrMaxD && x->r <= kRrMaxD && x->Rpad_b <= 512));
-  // rows per pass workgroup the LDS holds whole (both sides' widths)
-  const int sq_cap = !sq_sides ? 0
-                     : std::min(need_content ? sq_rows_cap(x->Dpad_b, std::min(B, kSqMaxB), x->Dpad) : kSqMaxRows,
-                                need_cf ? sq_rows_cap(x->Rpad_b, std::min(B, kSqMaxB), x->Rpad) : kSqMaxRows);
   if (sq_sel != 0 && x->dtype == F32 && B <= kSqMaxB && K_int <= kSqMaxK && sq_sides &&
-      x->n <= (int64_t)kSqMaxWg * sq_cap) {
+      x->n <= (int64_t)kSqMaxWg * kSqMaxRows) {
     static const int sq_wg_env = ab_env("BB_SQ_WG") ? atoi(ab_env("BB_SQ_WG")) : 256;
     const bool hyb = sides == 2;
     const int64_t wg_goal = std::max(1, std::min(sq_wg_env, kSqMaxWg));
-    const int32_t rpw = (int32_t)std::min<int64_t>(sq_cap, std::max<int64_t>(4, round_up((x->n + wg_goal - 1) / wg_goal, 4)));
+    const int32_t rpw = (int32_t)std::min<int64_t>(kSqMaxRows, std::max<int64_t>(4, round_up((x->n + wg_goal - 1) / wg_goal, 4)));
     const int32_t nwg = (int32_t)((x->n + rpw - 1) / rpw);
     const size_t top_side = (size_t)B * nwg * kSqM, ord_side = (size_t)B * x->n * 2;
     const size_t q_side = (size_t)B * kRrMaxD;
     if ((rc = x->sq_top.ensure(top_side * 8 * sides)) || (rc = x->sq_ptop.ensure(top_side * 8)) ||
-        (rc = x->sq_ords.ensure(ord_side * 4 * sides)) || (rc = x->sq_q.ensure(q_side * 4 * sides)) ||
+        (rc = x->sq_ords.ensure(ord_side * 4 * sides)) || (rc = x->sq_q.ensure((q_side + B) * 4 * sides)) ||
         (rc = x->keys.ensure((size_t)sides * B * K_int * 8)) || (rc = x->maxk.ensure((size_t)B * 8)))
       return rc;
     const bool host_res = !out_keys && res->where != BB_DEVICE;
@@ -777,9 +773,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       a.n = (int32_t)x->n;
       a.gid0 = (uint32_t)x->id_offset;
       a.present = (const uint32_t*)(cf_side ? x->cf_present.p : x->items_present.p);
-      a.mask = (const uint32_t*)d_mask;
-      a.excl = cf_side ? (const uint32_t*)d_excl : nullptr;  // rated items: the CF side only (as the scans)
-      a.excl_ld = nw;
+      a.mask = (const uint32_t*)(d_mask ? d_mask : x->ones.p);
+      // rated items: the CF side only (as the scans)
+      a.excl = (const uint32_t*)(cf_side && d_excl ? d_excl : x->zeros.p);
+      a.excl_ld = cf_side && d_excl ? nw : 0;
       a.drop = drop && side == 0;
       a.B = B;
       if (q->mode == BB_MODE_SEMANTIC || cf_side || !d_items) {
@@ -793,6 +790,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         a.q_id_offset = x->id_offset;
       }
       a.q_out = (float*)x->sq_q.p + side * q_side;
+      a.q_margin = (float*)x->sq_q.p + sides * q_side + side * B;
       a.rpw = rpw;
       a.nwg = nwg;
       a.K = K_int;

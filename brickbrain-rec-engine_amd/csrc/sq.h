@@ -29,8 +29,8 @@ struct SqArgs {
   int32_t n;
   uint32_t gid0;            // global id of row 0
   const uint32_t* present;  // local-row bitsets: the side's item space,
-  const uint32_t* mask;     //   the constraint mask (null = all),
-  const uint32_t* excl;     //   per-query exclusions [B][excl_ld] (null = none)
+  const uint32_t* mask;     //   the constraint mask (all ones: none),
+  const uint32_t* excl;     //   per-query exclusions [B][excl_ld] (none: all zeros, excl_ld 0)
   int64_t excl_ld;
   int32_t drop;             // rank-0 drop: keep the present candidates too
   int32_t B;
@@ -45,6 +45,7 @@ struct SqArgs {
   const int64_t* q_ids;
   int64_t q_id_offset;
   float* q_out;             // [B][ldx] the f32 query rows (written by workgroup 0) for the rescore
+  float* q_margin;          // [B] their re-rank margins 2δ (written by workgroup 0)
   int32_t rpw, nwg;         // rows per workgroup (multiple of 4), workgroups
   uint64_t* wg_top;         // [B][nwg][kSqM] eligible approximate keys (0 = empty)
   uint64_t* wg_ptop;        // [B][nwg][kSqM] present approximate keys (drop)
@@ -62,10 +63,6 @@ struct SqArgs {
   uint64_t* trace;          // probe runs (BB_SQ_TRACE): pass phase stamps [nwg][8], or null
   uint64_t* mtrace;         //   and merge phase stamps [B][8] of this side, or null
 };
-
-// rows per pass workgroup whose f16 rows (ldb wide), B query rows (ldx wide) and order images
-// fit the LDS at once (a multiple of 16, <= kSqMaxRows)
-int sq_rows_cap(int64_t ldb, int B, int64_t ldx);
 
 // the approximate pass, then the merge (a1 != null: both hybrid sides in one launch)
 hipError_t launch_sq_scan(const SqArgs& a, hipStream_t s);

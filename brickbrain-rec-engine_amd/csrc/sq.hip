@@ -6,11 +6,11 @@
 // one liked set (:612-677).  For such batches the MFMA scan + per-lane lists + list select of
 // the large-batch path is mostly latency; here (sq.h):
 //
-//   pass   workgroup blk stages rows [blk·rpw, +rpw) of the f16 copy into LDS by LDS-DMA
-//          (the whole block in flight at once) and scores them on the matrix cores against the
+//   pass   workgroup blk loads rows [blk·rpw, +rpw) of the f16 copy straight into registers
+//          (every load in flight at once) and scores them on the matrix cores against the
 //          query rows split into f16 hi + lo (16 queries per MFMA column block, f32
-//          accumulation): a = Σ x̃_j (h_j + l_j).  |a − s| <= δ (sq_margin) for the exact score s
-//          (E_x, N_x, Ñ_x = rr_stats).  Per query it leaves its top kSqM eligible (and present)
+//          accumulation): a = Σ x̃_j (h_j + l_j).  |a − s| <= δ (sq_margin_of) for the exact
+//          score s (E_x, N_x, Ñ_x = rr_stats).  Per query it leaves its top kSqM eligible (and present)
 //          approximate keys and every row's approximate order image.
 //   merge  one workgroup per query: L = a lower bound of the K-th largest workgroup maximum
 //          (16-bit prefix search: K distinct items reach it, so the exact K-th score is
@@ -32,24 +32,6 @@ namespace {
 constexpr int kSqThreads = 256;
 constexpr int kSqWaves = kSqThreads / 64;
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-
-// 16 B of LDS as four u32 (16-bit pairs).  (Read as a float vector, __builtin_bit_cast of its
-// .y/.z/.w elements compiled to a single ds_read_b32 whose .x stood in for all four on ROCm
-// 7.2 — wrong operands, not a fault.)
-__device__ __forceinline__ u4v lds_u4(const void* p, int c) {
-  return *(const __attribute__((address_space(3))) u4v*)((const __attribute__((address_space(3))) char*)((size_t)p) +
-                                                         c * 16);
-}
-
-
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t y = __shfl_xor(v, o);
-    v = v > y ? v : y;
-  }
-  return v;
-}
 
 // ballot compaction of `take` lanes' keys into cb[base..cap): returns the new base (uniform;
 // it keeps counting past cap)
@@ -152,14 +134,6 @@ __device__ __forceinline__ void sq_emit_any(const SqArgs& a, int b, const uint64
   else sq_emit<4>(a, b, cb, C, gmax);  // C <= kSqCand
 }
 
-// LDS-DMA of one 1-KiB piece (the wave's 64 lanes x 16 B, lane-linear at dst), M0 saved and
-// restored in the same statement (the compiler does not preserve it around inline asm)
-__device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-}
-
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
@@ -174,27 +148,55 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
                  c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
   return max(max(a, b), max(c, d));
 }
+// wave maximum of a u64: the high words, then the low words of the lanes holding that high word
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+  const uint32_t hi = wave_max_u32((uint32_t)(v >> 32));
+  const uint32_t lo = wave_max_u32((uint32_t)(v >> 32) == hi ? (uint32_t)v : 0u);
+  return ((uint64_t)hi << 32) | lo;
+}
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-// the query split of one 8-element k-group: hi = f16(v) and lo = f16(v − hi) (RNE,
-// saturating: to_f16), packed as the MFMA's B operands.  The merge recomputes both from the
-// f32 row for the bound (sq_margin), so nothing here is assumed about their accuracy.
+// The query split of one 8-element k-group as the MFMA's B operands: hi = f16(v) and lo =
+// f16(v − hi), both rounded toward zero (v_cvt_pkrtz_f16_f32: one instruction per pair, and
+// |hi| <= |v|, finite for finite v).  v − hi is exact in f32.  sq_margin_of bounds what the
+// split leaves out.
 __device__ __forceinline__ void split_f16x8(const float (&v)[8], u4v& hi, u4v& lo) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const uint16_t h0 = to_f16(v[2 * i]), h1 = to_f16(v[2 * i + 1]);
-    hi[i] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-    lo[i] = (uint32_t)to_f16(v[2 * i] - f16_val(h0)) | ((uint32_t)to_f16(v[2 * i + 1] - f16_val(h1)) << 16);
+    const auto h = __builtin_amdgcn_cvt_pkrtz(v[2 * i], v[2 * i + 1]);
+    hi[i] = __builtin_bit_cast(uint32_t, h);
+    lo[i] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(v[2 * i] - (float)h[0], v[2 * i + 1] - (float)h[1]));
   }
 }
 
-// Approximate pass on the matrix cores.  The workgroup's rows are staged into LDS by LDS-DMA
-// (the whole block in flight at once, one wait) in a chunk-major image: 16-row chunks, and in
-// a chunk the 16-B column cc of row r at slot cc·16 + r — one 1-KiB LDS-DMA piece (64 slots) per
-// four columns, and the MFMA operand of a 32-wide k-step is one contiguous, conflict-free
-// 1-KiB wave read.  Each wave scores whole chunks: per k-step two v_mfma_f32_16x16x32_f16 —
-// the f16 rows (A: 16 rows x 32) against the query rows split into f16 hi + lo (B: 32 x 16
-// queries, up to 16 per launch; |q − hi − lo| <= 2^-22·|q|), f32 accumulation.  KS = ldb / 32.
+// The re-rank margin 2δ (rr_margin) of one query row q (ldx wide; qn >= ‖q‖, qmax = max |q_j|),
+// with h, l the split above and r = q − h − l:
+//   δ = E_x·‖q‖ + Ñ_x·‖r‖ + γ·Ñ_x·(‖h‖ + ‖l‖) + 2^-23·N_x·‖q‖
+// — Σ(x̃_j − x_j)q_j by Cauchy–Schwarz (E_x); Σ x̃_j r_j, the split's residual; the f32
+// accumulation of the 2·ldb exact f16 products, Σ|x̃_j|(|h_j| + |l_j|) <= Ñ_x(‖h‖ + ‖l‖), over
+// 2·ldb/32 chained MFMAs of 32 products + the accumulator each, every one of the 33 values
+// rounded or truncated by at most 2^-23 of the largest partial sum whatever the matrix core's
+// order (γ = 33·(2·ldb/32)·2^-23); and the f32 rounding of s (2^-23·N_x).  Toward-zero f16
+// rounding is off by < 2^-10·|v| + 2^-24 (the subnormal spacing), so
+//   ‖h‖ <= ‖q‖,  ‖l‖ <= ‖q − h‖ <= 2^-10·‖q‖ + 2^-24·√ldx,  ‖r‖ <= 2^-20·‖q‖ + 2^-23·√ldx.
+// A row reaching the f16 range (|q_j| >= 2^15) gets an infinite margin: every item is then a
+// candidate (the merge's exact slow path).  E_x, N_x, Ñ_x = rr_stats of the side.
+__device__ __forceinline__ float sq_margin_of(const SqArgs& a, double qn, float qmax) {
+  if (!(qmax < 32768.f)) return __builtin_huge_valf();
+  const double rt = sqrt((double)a.ldx);
+  const double hl = qn * (1.0 + 0x1p-10) + 0x1p-24 * rt, rn = 0x1p-20 * qn + 0x1p-23 * rt;
+  const double gam = 33.0 * (2.0 * (double)a.ldb / 32.0) * 0x1p-23;
+  const double ex = (double)a.stats[0], nx = (double)a.stats[1], nxb = (double)a.stats[2];
+  const double d = ex * qn + nxb * rn + gam * nxb * hl + 0x1p-23 * nx * qn;
+  return rr_margin(__double2float_ru(d * (1.0 + 0x1p-20)));
+}
+
+// Approximate pass on the matrix cores.  Each wave scores whole 16-row chunks of the
+// workgroup's rows (chunks w, w + 4): it loads their f16 rows straight into registers as the
+// MFMA's A operands (lane l: row l & 15, bytes 64·ks + 16·(l >> 4) of k-step ks — two k-steps
+// read whole 128-B lines), so the rows never pass through LDS; per k-step two
+// v_mfma_f32_16x16x32_f16 against the query rows split into f16 hi + lo (B: 32 x 16 queries,
+// up to 16 per launch), f32 accumulation.  KS = ldb / 32.
 template <int KS>
 __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sq_smem[];
@@ -204,49 +206,74 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
   const int blk = blockIdx.x;
   const int r0 = blk * a.rpw, r1 = min(a.n, r0 + a.rpw), nr = r1 - r0;
   const int nck = (nr + 15) >> 4;
-  constexpr int CHB = 32 * 32 * KS;                   // bytes of a 16-row chunk (16 · ldb · 2)
-  char* rows = sq_smem;                               // [nck][CHB]
-  float* qs = (float*)(sq_smem + (size_t)nck * CHB);  // [B][ldx] f32 query rows
-  uint32_t* sel = (uint32_t*)(qs + B * ldx);          // [B][rpw] approximate order images
+  float* qs = (float*)sq_smem;               // [B][ldx] f32 query rows
+  uint32_t* sel = (uint32_t*)(qs + B * ldx);  // [B][rpw] approximate order images
   auto stamp = [&](int slot) {  // BB_SQ_TRACE probe runs: phase timeline (100 MHz), 8 words per workgroup
     if (a.trace && tid == 0) a.trace[(size_t)blk * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  {
-    const uint32_t rows_lds = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)rows);
-    const int r = lane & 15;
-    for (int c = 0; c < nck; ++c) {
-      const int row = 16 * c + r < nr ? r0 + 16 * c + r : r0;  // rows past the block: any valid row
-      const char* src_row = (const char*)a.Xb + (size_t)row * ldb * 2;
-      for (int P = w; P < KS; P += kSqWaves) {  // wave-uniform
-        const int cc = 4 * P + (lane >> 4);
-        glds16(src_row + cc * 16, __builtin_amdgcn_readfirstlane(rows_lds + (uint32_t)(c * CHB + P * 1024)));
-      }
-    }
-  }
-
   // query rows, as prep_kernel writes its f32 operand: normalised raw rows (qnorm.h), the
-  // stored rows of item ids, or CF rows as they are; zero past the row.  A wave's rows
-  // (b = w, w + 4, ...) are all loaded before any is used: one round trip, not one per row.
-  // Workgroup 0 also hands them to the merge (q_out).
+  // stored rows of item ids, or CF rows as they are; zero past the row.  Every query load of
+  // the wave (rows b = w, w + 4, ...) is issued before any is used, then this wave's chunks of
+  // item rows — unconditionally (a chunk past the block reloads row r0), so that the first use
+  // of a query element waits for the query loads only and leaves the chunks in flight (a branch
+  // between them would make the compiler drain everything).  Workgroup 0 also hands the rows
+  // to the merge (q_out) with their margins (q_margin).
   constexpr int QT = kSqMaxB / kSqWaves;
-  double xq[QT][kQnC];
+  constexpr int NCW = kSqMaxRows / 16 / kSqWaves;  // chunks per wave
+  u4v af[NCW][KS];
+  // the summary's eligibility words (item space, mask, per-query exclusions: every pointer
+  // valid, the host passes all-ones / all-zeros words for an absent mask / exclusion set)
+  constexpr int NE = kSqMaxRows / 64;
+  uint32_t wp[NE], wm[NE], wx[QT][NE];
+  auto load_rows = [&]() __attribute__((always_inline)) {
 #pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    const int b = w + kSqWaves * t;
-    if (b >= B) break;  // wave-uniform
-    if (a.q_kind == 1) {
-      const int64_t id = a.q_ids[b] - a.q_id_offset;
-      const bool ok = id >= 0 && id < a.n;
-      const float* src = a.X + (size_t)(ok ? id : 0) * ldx;
-      float v[kQnC];
+    for (int i = 0; i < NCW; ++i) {
+      const int rr = 16 * (w + kSqWaves * i) + (lane & 15);
+      const int row = r0 + (rr < nr ? rr : 0);
+      const u4v* src = (const u4v*)((const char*)a.Xb + (size_t)row * ldb * 2 + 16 * (lane >> 4));
 #pragma unroll
-      for (int c = 0; c < kQnC; ++c) v[c] = src[min(lane + 64 * c, ldx - 1)];
-#pragma unroll
-      for (int c = 0; c < kQnC; ++c) xq[t][c] = ok && lane + 64 * c < ldx ? (double)v[c] : 0.0;
-    } else {
-      load_chunk<kQnC>(a.q_src, a.q_dtype, (size_t)b * a.q_ld, 0, a.q_d, lane, xq[t]);
+      for (int ks = 0; ks < KS; ++ks) af[i][ks] = src[4 * ks];
     }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int row = min(r0 + lane + 64 * e, a.n - 1);
+      wp[e] = a.present[row >> 5];
+      wm[e] = a.mask[row >> 5];
+#pragma unroll
+      for (int t = 0; t < QT; ++t) wx[t][e] = a.excl[(size_t)min(w + kSqWaves * t, B - 1) * a.excl_ld + (row >> 5)];
+    }
+    asm volatile("" ::: "memory");  // the scheduler would sink these loads below the query's first use
+  };
+  double xq[QT][kQnC];
+  if (a.q_kind != 1 && a.q_dtype != F32) {  // (uniform) bf16 / f64 query rows: the generic loader
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+      load_chunk<kQnC>(a.q_src, a.q_dtype, (size_t)min(w + kSqWaves * t, B - 1) * a.q_ld, 0, a.q_d, lane, xq[t]);
+    load_rows();
+  } else {
+    int64_t qid[QT];
+    if (a.q_kind == 1) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t) qid[t] = a.q_ids[min(w + kSqWaves * t, B - 1)] - a.q_id_offset;
+    }
+    float qv[QT][kQnC];
+    bool qok[QT];
+    const int qlen = a.q_kind == 1 ? ldx : a.q_d;
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const int b = min(w + kSqWaves * t, B - 1);
+      qok[t] = a.q_kind != 1 || (qid[t] >= 0 && qid[t] < a.n);
+      const float* src = a.q_kind == 1 ? a.X + (size_t)(qok[t] ? qid[t] : 0) * ldx
+                                       : (const float*)a.q_src + (size_t)b * a.q_ld;
+#pragma unroll
+      for (int c = 0; c < kQnC; ++c) qv[t][c] = src[min(lane + 64 * c, qlen - 1)];
+    }
+    load_rows();
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int c = 0; c < kQnC; ++c) xq[t][c] = qok[t] && lane + 64 * c < qlen ? (double)qv[t][c] : 0.0;
   }
   stamp(1);
 #pragma unroll
@@ -254,51 +281,63 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
     const int b = w + kSqWaves * t;
     if (b >= B) break;
     const double nrm = a.q_kind == 0 ? qn_norm(xq[t]) : 1.0;
+    double ss = 0.0;
+    float mx = 0.f;
 #pragma unroll
     for (int c = 0; c < kQnC; ++c) {
       const int i = lane + 64 * c;
       if (i < ldx) {
         const float v = qn_elem(xq[t][c], nrm);
         qs[b * ldx + i] = v;
-        if (blk == 0) a.q_out[(size_t)b * ldx + i] = v;
+        if (blk == 0) {
+          a.q_out[(size_t)b * ldx + i] = v;
+          ss = fma((double)v, (double)v, ss);
+          mx = fmaxf(mx, fabsf(v));
+        }
       }
     }
+    if (blk == 0) {  // (workgroup-uniform)
+      ss = qn_wave_sum(ss);
+      mx = __int_as_float((int)wave_max_u32((uint32_t)__float_as_int(mx)));  // non-negative: bits order
+      if (lane == 0) a.q_margin[b] = sq_margin_of(a, sqrt(ss) * (1.0 + 0x1p-40), mx);
+    }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows' LDS-DMA has landed
   __syncthreads();
   stamp(2);
-  // the B operand: lane l holds query n = l & 15, k = 32·ks + 8·(l >> 4) + j, as f16 hi + lo
-  u4v qhi[KS], qlo[KS];
+  f4v acc[NCW];
+#pragma unroll
+  for (int i = 0; i < NCW; ++i) acc[i] = f4v{0.f, 0.f, 0.f, 0.f};
   {
     const int n = lane & 15;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+      // the B operand of k-step ks: lane l holds query n = l & 15, k = 32·ks + 8·(l >> 4) + j
       const int k0 = 32 * ks + 8 * (lane >> 4);
       const bool on = n < B && k0 < ldx;
       const f4v v0 = on ? lds_f4(qs + n * ldx, k0 >> 2) : f4v{0.f, 0.f, 0.f, 0.f};
       const f4v v1 = on ? lds_f4(qs + n * ldx, (k0 >> 2) + 1) : f4v{0.f, 0.f, 0.f, 0.f};
       const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      split_f16x8(v, qhi[ks], qlo[ks]);
+      u4v hi, lo;
+      split_f16x8(v, hi, lo);
+#pragma unroll
+      for (int i = 0; i < NCW; ++i) {
+        if (w + kSqWaves * i < nck) {  // wave-uniform
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[i][ks]),
+                                                          __builtin_bit_cast(f16x8, hi), acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[i][ks]),
+                                                          __builtin_bit_cast(f16x8, lo), acc[i], 0, 0, 0);
+        }
+      }
     }
   }
-  for (int c = w; c < nck; c += kSqWaves) {  // wave-uniform
-    const char* chunk = rows + c * CHB;
-    u4v af[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) af[ks] = lds_u4(chunk, ks * 64 + lane);
-    f4v acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[ks]), __builtin_bit_cast(f16x8, qhi[ks]),
-                                                   acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[ks]), __builtin_bit_cast(f16x8, qlo[ks]),
-                                                   acc, 0, 0, 0);
-    }
+  for (int i = 0; i < NCW; ++i) {
+    const int c = w + kSqWaves * i;
     const int n = lane & 15, rb = 16 * c + 4 * (lane >> 4);  // D: query n, rows rb .. rb + 3
-    if (n < B) {
+    if (c < nck && n < B) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (rb + i < nr) sel[n * a.rpw + rb + i] = ord_of(acc[i] + 0.0f);
+      for (int j = 0; j < 4; ++j)
+        if (rb + j < nr) sel[n * a.rpw + rb + j] = ord_of(acc[i][j] + 0.0f);
     }
   }
   __syncthreads();
@@ -307,23 +346,6 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
   // per query: eligibility, the order images of the rows, the top kSqM eligible (and present)
   // approximate keys.  The item-space and mask words are the same for every query: loaded once;
   // a wave's exclusion words for all its queries in one round.
-  constexpr int NE = kSqMaxRows / 64;
-  uint32_t wp[NE], wm[NE], wx[QT][NE];
-#pragma unroll
-  for (int e = 0; e < NE; ++e) {
-    const int row = min(r0 + lane + 64 * e, a.n - 1);
-    wp[e] = a.present[row >> 5];
-    wm[e] = a.mask ? a.mask[row >> 5] : 0xFFFFFFFFu;
-  }
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    const int b = w + kSqWaves * t;
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      const int row = min(r0 + lane + 64 * e, a.n - 1);
-      wx[t][e] = a.excl && b < B ? a.excl[(size_t)b * a.excl_ld + (row >> 5)] : 0u;
-    }
-  }
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
     const int b = w + kSqWaves * t;
@@ -373,44 +395,6 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
   stamp(4);
 }
 
-// the re-rank margin 2δ (rr_margin) of a query row, every lane of the wave (qrow: the f32 row,
-// ldx wide), with h, l the pass's f16 split of q and r = q − h − l (recomputed here in f64):
-//   δ = E_x·‖q‖ + Ñ_x·‖r‖ + γ·Ñ_x·(‖h‖ + ‖l‖) + 2^-23·N_x·‖q‖
-// — Σ(x̃_j − x_j)q_j by Cauchy–Schwarz (E_x); Σ x̃_j r_j (the split's residual); the f32
-// accumulation of the 2·ldb exact f16 products, Σ|x̃_j|(|h_j| + |l_j|) <= Ñ_x(‖h‖ + ‖l‖), over
-// 2·ldb/32 chained MFMAs of 32 products + the accumulator each, every one of the 33 values
-// rounded or truncated by at most 2^-23 of the largest partial sum whatever the matrix core's
-// order (γ = 33·(2·ldb/32)·2^-23); and the f32 rounding of s (2^-23·N_x).  E_x, N_x, Ñ_x =
-// rr_stats of the side.
-__device__ __forceinline__ float sq_margin(const SqArgs& a, const float* qrow) {
-  const int lane = threadIdx.x & 63, ldx = (int)a.ldx;
-  float v[kQnC];
-#pragma unroll
-  for (int c = 0; c < kQnC; ++c) v[c] = qrow[min(lane + 64 * c, ldx - 1)];
-  double qq = 0.0, rr = 0.0, hh = 0.0, ll = 0.0;
-#pragma unroll
-  for (int c = 0; c < kQnC; ++c) {
-    const float x = lane + 64 * c < ldx ? v[c] : 0.f;
-    const double h = (double)f16_val(to_f16(x));
-    const double l = (double)f16_val(to_f16(x - (float)h));
-    const double r = (double)x - h - l;
-    qq = fma((double)x, (double)x, qq);
-    rr = fma(r, r, rr);
-    hh = fma(h, h, hh);
-    ll = fma(l, l, ll);
-  }
-  qq = qn_wave_sum(qq);
-  rr = qn_wave_sum(rr);
-  hh = qn_wave_sum(hh);
-  ll = qn_wave_sum(ll);
-  const double up = 1.0 + 0x1p-40;
-  const double qn = sqrt(qq) * up, rn = sqrt(rr) * up, sn = (sqrt(hh) + sqrt(ll)) * up;
-  const double gam = 33.0 * (2.0 * (double)a.ldb / 32.0) * 0x1p-23;
-  const double ex = (double)a.stats[0], nx = (double)a.stats[1], nxb = (double)a.stats[2];
-  const double d = ex * qn + nxb * rn + gam * nxb * sn + 0x1p-23 * nx * qn;
-  return rr_margin(__double2float_ru(d * (1.0 + 0x1p-20)));
-}
-
 // Candidates of one query by one wave from the workgroups' lists of kSqM approximate keys
 // (tops: [nwg][kSqM]): the bound is the K-th largest list maximum's 16-bit prefix (kth) or
 // the largest maximum (rank 0), minus the margin (computed here from qrow while the list loads
@@ -418,7 +402,7 @@ __device__ __forceinline__ float sq_margin(const SqArgs& a, const float* qrow) {
 // workgroup whose kSqM-th key reaches it that its list did not hold.  Returns the count (it
 // may exceed cap: the caller's slow path) and the bound.
 template <int NL>  // nwg <= 64·NL
-__device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint32_t* ords, int K, const float* qrow,
+__device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint32_t* ords, int K, const float* mp,
                               bool kth, uint64_t* cb, uint32_t cap, uint32_t* T_out) {
   const int lane = threadIdx.x & 63;
   const int nwg = a.nwg;
@@ -429,7 +413,7 @@ __device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* t
 #pragma unroll
     for (int j = 0; j < kSqM; ++j) ent[i][j] = t < nwg ? tops[(size_t)t * kSqM + j] : 0ull;
   }
-  const float margin = sq_margin(a, qrow);
+  const float margin = *mp;
   uint32_t top;
   if (kth) {  // the largest multiple of 2^16 with >= K workgroup maxima at or above it
     uint32_t prefix = 0;
@@ -442,10 +426,10 @@ __device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* t
     }
     top = prefix;
   } else {  // the largest maximum (rank 0)
-    uint64_t m = 0;
+    uint32_t m = 0;
 #pragma unroll
-    for (int i = 0; i < NL; ++i) m = m > ent[i][0] ? m : ent[i][0];
-    top = ordk_of(wave_max_u64(m));
+    for (int i = 0; i < NL; ++i) m = max(m, ordk_of(ent[i][0]));
+    top = wave_max_u32(m);
   }
   const uint32_t T = top ? ord_sub(top, margin) : 1u;
   *T_out = T;
@@ -566,6 +550,7 @@ __device__ __forceinline__ void sq_merge_row(const SqArgs& a, int b, SqMergeLds&
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int ldx = (int)a.ldx;
   const float* qrow = a.q_out + (size_t)b * ldx;
+  const float* mp = a.q_margin + b;
   auto stamp = [&](int slot) {  // BB_SQ_TRACE probe runs: phase timeline (100 MHz)
     if (a.mtrace && tid == 0) a.mtrace[(size_t)b * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
@@ -575,16 +560,16 @@ __device__ __forceinline__ void sq_merge_row(const SqArgs& a, int b, SqMergeLds&
     uint32_t T;
     const uint64_t* tops = a.wg_top + (size_t)b * a.nwg * kSqM;
     const uint32_t* ords = a.ords + (size_t)b * a.ords_ld;
-    const uint32_t ce = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, a.K, qrow, true, cand, kSqCand, &T)
-                                                      : sq_gather<8>(a, tops, ords, a.K, qrow, true, cand, kSqCand, &T);
+    const uint32_t ce = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, a.K, mp, true, cand, kSqCand, &T)
+                                                      : sq_gather<8>(a, tops, ords, a.K, mp, true, cand, kSqCand, &T);
     if (lane == 0) misc[0] = ce, misc[2] = T;
   } else if (w == 1) {
     uint32_t T = 0xFFFFFFFFu, cp = 0;
     if (a.drop) {
       const uint64_t* tops = a.wg_ptop + (size_t)b * a.nwg * kSqM;
       const uint32_t* ords = a.ords_p + (size_t)b * a.ords_ld;
-      cp = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, 1, qrow, false, ptmp, kSqPCand, &T)
-                                        : sq_gather<8>(a, tops, ords, 1, qrow, false, ptmp, kSqPCand, &T);
+      cp = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, 1, mp, false, ptmp, kSqPCand, &T)
+                                        : sq_gather<8>(a, tops, ords, 1, mp, false, ptmp, kSqPCand, &T);
     }
     if (lane == 0) misc[1] = cp, misc[3] = T;
   }
@@ -622,35 +607,19 @@ __global__ __launch_bounds__(kSqThreads) void sq_merge_kernel(SqArgs a0, SqArgs 
 
 template <int KS>
 hipError_t launch_sq_ks(const SqArgs& a, hipStream_t s) {
-  const int nck = (a.rpw + 15) / 16;
-  const size_t lds = (size_t)nck * 32 * 32 * KS + (size_t)a.B * a.ldx * 4 + (size_t)a.B * a.rpw * 4;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  // dynamic LDS beyond 64 KiB needs the per-kernel opt-in, at the size launched (grows only)
-  static size_t allowed = 64 * 1024;
-  if (lds > allowed) {
-    const hipError_t e = hipFuncSetAttribute((const void*)sq_scan_kernel<KS>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    allowed = lds;
-  }
+  const size_t lds = (size_t)a.B * a.ldx * 4 + (size_t)a.B * a.rpw * 4;  // <= 40 KiB
   hipLaunchKernelGGL(sq_scan_kernel<KS>, dim3(a.nwg), dim3(kSqThreads), lds, s, a);
   return hipGetLastError();
 }
 
 }  // namespace
 
-int sq_rows_cap(int64_t ldb, int B, int64_t ldx) {
-  const int64_t avail = 160 * 1024 - (int64_t)B * ldx * 4;
-  int rows = kSqMaxRows;
-  while (rows > 16 && (int64_t)(rows / 16) * 32 * ldb + (int64_t)B * rows * 4 > avail) rows -= 16;
-  return rows;
-}
-
 hipError_t launch_sq_scan(const SqArgs& a, hipStream_t s) {
   if (a.B < 1 || a.B > kSqMaxB || a.ldx > kRrMaxD || (a.ldx & 31) || a.ldb < a.ldx || (a.ldb & 63) || a.ldb > 512 ||
       a.K < 1 || a.K > kSqMaxK || a.rpw < 4 || (a.rpw & 3) || a.rpw > kSqMaxRows || a.nwg < 1 || a.nwg > kSqMaxWg ||
       (int64_t)a.nwg * a.rpw < a.n || (int64_t)(a.nwg - 1) * a.rpw >= a.n || a.n < 1 || a.ords_ld < a.n ||
-      !a.present || !a.Xb || !a.X || !a.stats || !a.q_out || (a.drop && (!a.ords_p || !a.wg_ptop)))
+      !a.present || !a.mask || !a.excl || a.excl_ld < 0 || !a.Xb || !a.X || !a.stats || !a.q_out || !a.q_margin ||
+      (a.drop && (!a.ords_p || !a.wg_ptop)))
     return hipErrorInvalidValue;
   switch (a.ldb / 32) {
     case 2: return launch_sq_ks<2>(a, s);

@@ -39,6 +39,20 @@ def main():
                 ev.append((a, e))
                 torch.cuda.synchronize()   # one at a time: idle before each
             out[f"v{v}_B{B}"] = round(float(np.median([a.elapsed_time(e) for a, e in ev])) * 1e3, 2)
+            if os.environ.get("SQ_PROBE_GRAPH"):  # the same search captured once, replayed
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    run()
+                torch.cuda.synchronize()
+                ev = []
+                for _ in range(200):
+                    a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(s)
+                    g.replay()
+                    e.record(s)
+                    ev.append((a, e))
+                    torch.cuda.synchronize()
+                out[f"v{v}_B{B}_graph"] = round(float(np.median([a.elapsed_time(e) for a, e in ev])) * 1e3, 2)
     print(json.dumps(out))
 
 
