@@ -117,7 +117,7 @@ class ItemIndex:
             if not getattr(self, "_h", None):
                 return
             if getattr(self, "_views", 0):
-                raise L.BrickrecError("close this index's views and captured searches first")
+                raise L.BrickrecError("close this index's views first")
             L.check(self._lib.bb_destroy(self._h), "bb_destroy")
             self._h = None
         base = getattr(self, "_base", None)
@@ -325,51 +325,6 @@ class ItemIndex:
                 L.check(rc, "bb_search")
         run._keep = (keep, q, res)  # keep buffers and structs alive with the closure
         return run, out
-
-    def captured_search(self, mode: str, k: int, *, q_rows=None, q_items=None, q_cf=None,
-                        mask=None, excl=None, k_side: int = 0, w_content=0.4, w_cf=0.6, stream=None):
-        """The search captured once as a HIP graph (bb_graph_create) on a private view, for
-        repeated one-query requests: refill the same input tensors, call replay() (one
-        hipGraphLaunch), read the same outputs.  Inputs as prepared_search; stream must not be
-        the null stream.  Returns (replay, outputs, close)."""
-        import torch
-        first = next(x for x in (q_rows, q_items, q_cf) if x is not None)
-        dev, B = first.device, int(first.shape[0])
-        out = (torch.empty((B, k), dtype=torch.float32, device=dev),
-               torch.empty((B, k), dtype=torch.int64, device=dev),
-               torch.empty((B,), dtype=torch.int32, device=dev))
-        s = stream if stream is not None else torch.cuda.Stream(dev)
-        keep = [t for t in (q_rows, q_items, q_cf, mask, excl) if t is not None]
-        q = self._query(mode, k, B, k_side, L.BB_DEVICE,
-                        q_rows.data_ptr() if q_rows is not None else None,
-                        _torch_dtype_code(q_rows) if q_rows is not None else 0,
-                        q_items.data_ptr() if q_items is not None else None,
-                        q_cf.data_ptr() if q_cf is not None else None,
-                        _torch_dtype_code(q_cf) if q_cf is not None else 0,
-                        mask.data_ptr() if mask is not None else None,
-                        excl.data_ptr() if excl is not None else None, w_content, w_cf, s.cuda_stream, 0)
-        res = L.bb_result(out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), L.BB_DEVICE, None, None)
-        g = C.c_void_p()
-        with self._mu:
-            L.check(self._lib.bb_graph_create(self._h, C.byref(q), C.byref(res), C.byref(g)), "bb_graph_create")
-            self._views = getattr(self, "_views", 0) + 1  # a graph holds a private view of the rows
-        fn, gp = self._lib.bb_graph_launch, g
-
-        def replay():
-            rc = fn(gp, None)
-            if rc:
-                L.check(rc, "bb_graph_launch")
-
-        def close():
-            with self._mu:
-                if replay._g is not None:
-                    L.check(self._lib.bb_graph_destroy(replay._g), "bb_graph_destroy")
-                    replay._g = None
-                    self._views -= 1
-
-        replay._keep = (keep, q, res, s)
-        replay._g = g
-        return replay, out, close
 
     # ------------------------------------------------------------------ sharded search
     def key_lens(self, mode: str, k: int, k_side: int = 0) -> Tuple[int, int]:

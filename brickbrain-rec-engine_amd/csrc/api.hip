@@ -1629,75 +1629,6 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
 
 extern "C" {
 
-// ---- captured searches (bb_graph_*) ----
-struct bb_graph {
-  bb_index* view = nullptr;  // private workspace: the captured pointers stay valid
-  hipStream_t stream = nullptr;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-};
-
-int bb_graph_destroy(bb_graph* g) {
-  if (!g) return BB_OK;
-  int rc = BB_OK;
-  if (g->view) {
-    DeviceGuard dg(g->view->device);
-    if (g->exec) (void)hipStreamSynchronize(g->stream);
-    if (g->exec) (void)hipGraphExecDestroy(g->exec);
-    if (g->graph) (void)hipGraphDestroy(g->graph);
-    rc = bb_destroy(g->view);
-  }
-  delete g;
-  return rc;
-}
-
-int bb_graph_create(bb_index* base, const bb_query* q, bb_result* res, bb_graph** out) {
-  if (!base || !q || !res || !out) return fail(BB_E_ARG, "bb_graph_create: null argument");
-  *out = nullptr;
-  if (q->where != BB_DEVICE || res->where != BB_DEVICE || !q->stream)
-    return fail(BB_E_ARG, "bb_graph_create: device inputs, device results and a non-null stream are required");
-  if (base->prof) return fail(BB_E_STATE, "bb_graph_create: profiling is on");
-  bb_graph* g = new bb_graph();
-  g->stream = (hipStream_t)q->stream;
-  int rc = bb_create_view(base, &g->view);  // (it takes the base's search options)
-  // one plain search first: the view's workspace reaches its size (no allocation in capture)
-  if (rc == BB_OK) rc = bb_search(g->view, q, res);
-  if (rc == BB_OK) {
-    bb_index* x = g->view;
-    std::lock_guard<std::mutex> lk(x->mu);
-    DeviceGuard dg(x->device);
-    if (hipStreamSynchronize(g->stream) != hipSuccess ||
-        hipStreamBeginCapture(g->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-      rc = fail(BB_E_HIP, "bb_graph_create: cannot begin capture on the stream");
-    } else {
-      rc = search_locked(x, q, res, true);
-      hipGraph_t graph = nullptr;
-      const hipError_t e = hipStreamEndCapture(g->stream, &graph);
-      g->graph = graph;
-      if (rc == BB_OK && e != hipSuccess)
-        rc = fail(BB_E_STATE, std::string("bb_graph_create: this search cannot be captured: ") + hipGetErrorString(e));
-      else if (rc != BB_OK)
-        rc = fail(BB_E_STATE, std::string("bb_graph_create: this search cannot be captured: ") + bb_last_error());
-      if (rc == BB_OK && hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0) != hipSuccess)
-        rc = fail(BB_E_HIP, "bb_graph_create: hipGraphInstantiate failed");
-    }
-  }
-  if (rc != BB_OK) {
-    (void)hipGetLastError();  // a refused call inside the capture leaves a sticky-free error
-    bb_graph_destroy(g);
-    return rc;
-  }
-  *out = g;
-  return BB_OK;
-}
-
-int bb_graph_launch(bb_graph* g, void* stream) {
-  if (!g || !g->exec) return fail(BB_E_ARG, "bb_graph_launch: no graph");
-  DeviceGuard dg(g->view->device);
-  BB_HIP(hipGraphLaunch(g->exec, stream ? (hipStream_t)stream : g->stream));
-  return BB_OK;
-}
-
 int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
   if (!x || !q || !res) return fail(BB_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(x->mu);

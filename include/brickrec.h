@@ -203,7 +203,7 @@ int bb_get_profile(bb_index* idx, bb_profile* out);
  *                           identical either way.
  *   BB_OPT_SMALL_BATCH      -1 auto (default, = 1), 0 off: batches of up to 16 query rows (any
  *                           mode, hybrid included) on an f32 index of up to 65,536 rows take
- *                           one approximate pass over the f16 copy per side and an exact
+ *                           one approximate pass over the bf16 copy per side and an exact
  *                           rescore of the candidates within its proven bound (no MFMA scan,
  *                           lists or list select) — the reference's one-query request shape.
  *                           Results are identical either way. */
@@ -229,21 +229,6 @@ int bb_get_rows(bb_index* idx, const int64_t* ids, int32_t B, void* out, int32_t
  * with ONE copy of the index in HBM / the MALL instead of one per in-flight handle.  Uploads to
  * a view, or to a base while it has views, fail with BB_E_STATE; destroy the views first. */
 int bb_create_view(bb_index* base, bb_index** out);
-
-/* A search captured once as a HIP graph and replayed (no reference counterpart: serving
- * plumbing for the reference's one-query request shape, where host launch overhead is a large
- * part of the latency).  q and res must be all-device (BB_DEVICE, q->stream a non-null stream);
- * the graph keeps reading q's input pointers and writing res's output pointers, so a caller
- * fills the same query buffers and replays.  The graph runs on a private view of `base` (its
- * own workspace, so later searches on the base never move the buffers the graph uses): the
- * base cannot take uploads while graphs exist.  A search whose path needs the host between
- * launches (streaming overflow reruns, host-side results) fails with BB_E_STATE; so does
- * capture with profiling on.  bb_graph_launch enqueues one replay on `stream` (NULL: the
- * captured stream). */
-typedef struct bb_graph bb_graph;
-int bb_graph_create(bb_index* base, const bb_query* q, bb_result* res, bb_graph** out);
-int bb_graph_launch(bb_graph* g, void* stream);
-int bb_graph_destroy(bb_graph* g);
 
 int bb_info(bb_index* idx, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* r);
 int bb_destroy(bb_index* idx);

@@ -305,35 +305,3 @@ def test_device_inputs_and_views(c1, brickrec):
         assert np.array_equal(out[0].cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
     finally:
         v.close()
-
-
-def test_captured_search_replays(c1, brickrec):
-    """bb_graph_create: the one-query search captured once as a HIP graph on a private view;
-    refilling the same input tensors and replaying gives exactly the direct search's lists,
-    for semantic rows and for similar-sets ids (small-batch path), and for a 256-row batch
-    (large-batch path: prep + scan + list select)."""
-    import torch
-    idx, x, rows = c1
-    dev = torch.device("cuda", 0)
-    cases = [("semantic", 20, dict(q_rows=torch.from_numpy(R.unit_rows(1, 384, 901)).to(dev))),
-             ("similar", 10, dict(q_items=torch.tensor([4242], dtype=torch.int64, device=dev))),
-             ("semantic", 50, dict(q_rows=torch.from_numpy(R.unit_rows(256, 384, 902)).to(dev)))]
-    for mode, k, kw in cases:
-        replay, out, close = idx.captured_search(mode, k, **kw)
-        try:
-            for rep in range(3):
-                name, t = next(iter(kw.items()))
-                if rep:  # new request contents in the same buffers
-                    if name == "q_rows":
-                        t.copy_(torch.from_numpy(R.unit_rows(t.shape[0], 384, 903 + rep)).to(dev))
-                    else:
-                        t.fill_(100 * rep + 7)
-                    torch.cuda.synchronize()  # (the graph runs on its own stream)
-                replay()
-                torch.cuda.synchronize()
-                ref = idx.search(mode, k, **{name: t.cpu().numpy()})
-                assert np.array_equal(out[1].cpu().numpy(), ref[1])
-                assert np.array_equal(out[0].cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
-                assert np.array_equal(out[2].cpu().numpy(), ref[2])
-        finally:
-            close()

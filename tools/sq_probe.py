@@ -53,21 +53,6 @@ def main():
                     ev.append((a, e))
                     torch.cuda.synchronize()
                 out[f"v{v}_B{B}_graph"] = round(float(np.median([a.elapsed_time(e) for a, e in ev])) * 1e3, 2)
-                # the library's own capture (bb_graph_create on a private view), on its stream
-                replay, _, close = idx.captured_search("semantic", k, q_rows=q, stream=s)
-                for _ in range(20):
-                    replay()
-                torch.cuda.synchronize()
-                ev = []
-                for _ in range(200):
-                    a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    a.record(s)
-                    replay()
-                    e.record(s)
-                    ev.append((a, e))
-                    torch.cuda.synchronize()
-                out[f"v{v}_B{B}_bbgraph"] = round(float(np.median([a.elapsed_time(e) for a, e in ev])) * 1e3, 2)
-                close()
     print(json.dumps(out))
 
 
