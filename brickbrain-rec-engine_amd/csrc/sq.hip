@@ -89,17 +89,9 @@ __device__ __forceinline__ void sq_emit(const SqArgs& a, int b, const uint64_t* 
 
 // The same result for C <= 64 keys without a sorting network: the keys are distinct (ids), so
 // lane l's rank is the number of larger keys, counted against each key broadcast in turn.
-__device__ __forceinline__ void sq_emit_rank(const SqArgs& a, int b, const uint64_t* cb, int C, uint64_t gmax) {
+// write the C <= 64 keys v (lane < C) at their ranks r
+__device__ __forceinline__ void sq_emit_ranked(const SqArgs& a, int b, uint64_t v, int r, int C, uint64_t gmax) {
   const int lane = threadIdx.x & 63;
-  const uint64_t v = lane < C ? cb[lane] : 0ull;
-  const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
-  int r = 0;
-  for (int j = 0; j < C; ++j) {  // uniform
-    // (readlane returns int: each half goes through uint32_t, or the low one sign-extends)
-    const uint64_t y = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, j) << 32) |
-                       (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vlo, j);
-    r += y > v;
-  }
   const bool on = lane < C;
   const int cnt = C < a.K ? C : a.K;
   if (a.out_scores) {
@@ -125,6 +117,14 @@ __device__ __forceinline__ void sq_emit_rank(const SqArgs& a, int b, const uint6
   if (on && r < cnt) out[r] = v;
   for (int e = cnt + lane; e < a.K; e += 64) out[e] = 0ull;
   if (lane == 0 && a.max_out) a.max_out[b] = a.drop ? gmax : 0ull;
+}
+
+__device__ __forceinline__ void sq_emit_rank(const SqArgs& a, int b, const uint64_t* cb, int C, uint64_t gmax) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t v = lane < C ? cb[lane] : 0ull;
+  int r = 0;
+  for (int j = 0; j < C; ++j) r += cb[j] > v;  // (uniform; one broadcast LDS read per key)
+  sq_emit_ranked(a, b, v, r, C, gmax);
 }
 
 __device__ __forceinline__ void sq_emit_any(const SqArgs& a, int b, const uint64_t* cb, int C, uint64_t gmax) {
@@ -276,31 +276,72 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
       for (int c = 0; c < kQnC; ++c) xq[t][c] = qok[t] && lane + 64 * c < qlen ? (double)qv[t][c] : 0.0;
   }
   stamp(1);
+  // this wave's queries (b = w + 4t, t < nq): norms with their butterflies interleaved across
+  // the rows (per row the operations and order of qn_norm: the same bits), then the f32 rows
+  const int nq = B > w ? (B - w + kSqWaves - 1) / kSqWaves : 0;  // (wave-uniform)
+  auto norm_rows = [&](auto NQC) __attribute__((always_inline)) {
+    constexpr int NQ = decltype(NQC)::value;
+    double nrm[NQ];
+    if (a.q_kind == 0) {
+      double s2[NQ];
 #pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    const int b = w + kSqWaves * t;
-    if (b >= B) break;
-    const double nrm = a.q_kind == 0 ? qn_norm(xq[t]) : 1.0;
-    double ss = 0.0;
-    float mx = 0.f;
+      for (int t = 0; t < NQ; ++t) {
+        s2[t] = 0.0;
 #pragma unroll
-    for (int c = 0; c < kQnC; ++c) {
-      const int i = lane + 64 * c;
-      if (i < ldx) {
-        const float v = qn_elem(xq[t][c], nrm);
-        qs[b * ldx + i] = v;
-        if (blk == 0) {
-          a.q_out[(size_t)b * ldx + i] = v;
-          ss = fma((double)v, (double)v, ss);
-          mx = fmaxf(mx, fabsf(v));
+        for (int c = 0; c < kQnC; ++c) s2[t] = fma(xq[t][c], xq[t][c], s2[t]);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) s2[t] += __shfl_xor(s2[t], o);
+#pragma unroll
+      for (int t = 0; t < NQ; ++t) {
+        const double r = sqrt(s2[t]);
+        nrm[t] = r == 0.0 ? 1.0 : r;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NQ; ++t) nrm[t] = 1.0;
+    }
+    double ss[NQ];
+    float mx[NQ];
+#pragma unroll
+    for (int t = 0; t < NQ; ++t) {
+      const int b = w + kSqWaves * t;
+      ss[t] = 0.0;
+      mx[t] = 0.f;
+#pragma unroll
+      for (int c = 0; c < kQnC; ++c) {
+        const int i = lane + 64 * c;
+        if (i < ldx) {
+          const float v = qn_elem(xq[t][c], nrm[t]);
+          qs[b * ldx + i] = v;
+          if (blk == 0) {
+            a.q_out[(size_t)b * ldx + i] = v;
+            ss[t] = fma((double)v, (double)v, ss[t]);
+            mx[t] = fmaxf(mx[t], fabsf(v));
+          }
         }
       }
     }
-    if (blk == 0) {  // (workgroup-uniform)
-      ss = qn_wave_sum(ss);
-      mx = __int_as_float((int)wave_max_u32((uint32_t)__float_as_int(mx)));  // non-negative: bits order
-      if (lane == 0) a.q_margin[b] = sq_margin_of(a, sqrt(ss) * (1.0 + 0x1p-40), mx);
+    if (blk == 0) {  // (workgroup-uniform) the margins
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) ss[t] += __shfl_xor(ss[t], o);
+#pragma unroll
+      for (int t = 0; t < NQ; ++t) {
+        const float m = __int_as_float((int)wave_max_u32((uint32_t)__float_as_int(mx[t])));  // non-negative: bits order
+        if (lane == 0) a.q_margin[w + kSqWaves * t] = sq_margin_of(a, sqrt(ss[t]) * (1.0 + 0x1p-40), m);
+      }
     }
+  };
+  switch (nq) {
+    case 1: norm_rows(std::integral_constant<int, 1>{}); break;
+    case 2: norm_rows(std::integral_constant<int, 2>{}); break;
+    case 3: norm_rows(std::integral_constant<int, 3>{}); break;
+    case 4: norm_rows(std::integral_constant<int, 4>{}); break;
+    default: break;
   }
   __syncthreads();
   stamp(2);
@@ -344,53 +385,74 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
   stamp(3);
 
   // per query: eligibility, the order images of the rows, the top kSqM eligible (and present)
-  // approximate keys.  The item-space and mask words are the same for every query: loaded once;
-  // a wave's exclusion words for all its queries in one round.
+  // approximate keys — the wave's queries side by side, so their wave-maximum chains (DPP +
+  // readlane) interleave instead of running one after another
+  auto summary = [&](auto NQC) __attribute__((always_inline)) {
+    constexpr int NQ = decltype(NQC)::value;
+    uint32_t o[NQ][NE], op[NQ][NE];
 #pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    const int b = w + kSqWaves * t;
-    if (b >= B) break;  // wave-uniform
-    uint32_t o[NE], op[NE];
+    for (int t = 0; t < NQ; ++t) {
+      const int b = w + kSqWaves * t;
 #pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      const int i = lane + 64 * e, row = r0 + i;
-      const uint32_t raw = i < nr ? sel[b * a.rpw + i] : 0u;
-      const uint32_t bit = 1u << (row & 31);
-      const bool pres = i < nr && (wp[e] & bit);
-      const bool elig = pres && (wm[e] & bit) && !(wx[t][e] & bit);
-      o[e] = elig ? raw : 0u;
-      op[e] = a.drop && pres ? raw : 0u;
-      if (i < nr) {
-        a.ords[(size_t)b * a.ords_ld + row] = o[e];
-        if (a.drop) a.ords_p[(size_t)b * a.ords_ld + row] = op[e];
+      for (int e = 0; e < NE; ++e) {
+        const int i = lane + 64 * e, row = r0 + i;
+        const uint32_t raw = i < nr ? sel[b * a.rpw + i] : 0u;
+        const uint32_t bit = 1u << (row & 31);
+        const bool pres = i < nr && (wp[e] & bit);
+        const bool elig = pres && (wm[e] & bit) && !(wx[t][e] & bit);
+        o[t][e] = elig ? raw : 0u;
+        op[t][e] = a.drop && pres ? raw : 0u;
+        if (i < nr) {
+          a.ords[(size_t)b * a.ords_ld + row] = o[t][e];
+          if (a.drop) a.ords_p[(size_t)b * a.ords_ld + row] = op[t][e];
+        }
       }
     }
     for (int set = 0; set < (a.drop ? 2 : 1); ++set) {  // wave-uniform
-      uint32_t(&oo)[NE] = set ? op : o;
-      uint64_t mine = 0;
+      uint64_t mine[NQ];
+#pragma unroll
+      for (int t = 0; t < NQ; ++t) mine[t] = 0;
 #pragma unroll
       for (int tt = 0; tt < kSqM; ++tt) {
         // the largest remaining order image; among equal ones the lowest row (largest key)
-        uint32_t lm = 0;
+        uint32_t m[NQ];
 #pragma unroll
-        for (int e = 0; e < NE; ++e) lm = max(lm, oo[e]);
-        const uint32_t m = wave_max_u32(lm);
-        uint64_t key = 0;
-        if (m) {
+        for (int t = 0; t < NQ; ++t) {
+          uint32_t lm = 0;
 #pragma unroll
-          for (int e = 0; e < NE; ++e) {
-            const uint64_t hit = __ballot(oo[e] == m);
-            if (hit && !key) {
-              const int src = __ffsll((unsigned long long)hit) - 1;
-              key = make_key(m, a.gid0 + (uint32_t)(r0 + src + 64 * e));
-              if (lane == src) oo[e] = 0u;
+          for (int e = 0; e < NE; ++e) lm = max(lm, set ? op[t][e] : o[t][e]);
+          m[t] = wave_max_u32(lm);
+        }
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) {
+          uint32_t(&oo)[NE] = set ? op[t] : o[t];
+          uint64_t key = 0;
+          if (m[t]) {
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+              const uint64_t hit = __ballot(oo[e] == m[t]);
+              if (hit && !key) {
+                const int src = __ffsll((unsigned long long)hit) - 1;
+                key = make_key(m[t], a.gid0 + (uint32_t)(r0 + src + 64 * e));
+                if (lane == src) oo[e] = 0u;
+              }
             }
           }
+          if (lane == tt) mine[t] = key;
         }
-        if (lane == tt) mine = key;
       }
-      if (lane < kSqM) (set ? a.wg_ptop : a.wg_top)[((size_t)b * a.nwg + blk) * kSqM + lane] = mine;
+#pragma unroll
+      for (int t = 0; t < NQ; ++t)
+        if (lane < kSqM)
+          (set ? a.wg_ptop : a.wg_top)[((size_t)(w + kSqWaves * t) * a.nwg + blk) * kSqM + lane] = mine[t];
     }
+  };
+  switch (nq) {
+    case 1: summary(std::integral_constant<int, 1>{}); break;
+    case 2: summary(std::integral_constant<int, 2>{}); break;
+    case 3: summary(std::integral_constant<int, 3>{}); break;
+    case 4: summary(std::integral_constant<int, 4>{}); break;
+    default: break;
   }
   stamp(4);
 }
@@ -537,6 +599,7 @@ struct SqMergeLds {
   uint64_t run[kSqMaxK];
   uint32_t scan_sh[kSelectThreads / 64];
   uint32_t misc[8];
+  int32_t rank[kSqWaves][64];
 };
 
 // Merge of query b of one side (a: a kernel argument itself, so its fields stay scalar loads)
@@ -587,13 +650,26 @@ __device__ __forceinline__ void sq_merge_row(const SqArgs& a, int b, SqMergeLds&
   sq_rescore(a, cand, (int)(ce + cp), qs);
   __syncthreads();
   stamp(2);
-  if (w == 0) {
+  const int C = (int)ce;
+  if (C <= 64 && (a.mopt & 2)) {
+    // rank counting on all four waves: wave w compares against keys [16w, 16w + 16)
+    const uint64_t v = lane < C ? cand[lane] : 0ull;
+    int r = 0;
+    for (int j = 16 * w; j < min(C, 16 * w + 16); ++j) r += cand[j] > v;  // (uniform)
+    L.rank[w][lane] = r;
+    __syncthreads();
+    if (w == 0) {
+      uint64_t gm = lane < (int)cp ? cand[C + lane] : 0ull;  // cp <= kSqPCand = 64
+      gm = wave_max_u64(gm);
+      sq_emit_ranked(a, b, v, L.rank[0][lane] + L.rank[1][lane] + L.rank[2][lane] + L.rank[3][lane], C, gm);
+    }
+  } else if (w == 0) {
     uint64_t gm = 0;
     for (int i = lane; i < (int)cp; i += 64) gm = gm > cand[ce + i] ? gm : cand[ce + i];
     gm = wave_max_u64(gm);
-    sq_emit_any(a, b, cand, (int)ce, gm);
-    if (a.mtrace && lane == 0) a.mtrace[(size_t)b * 8 + 4] = ce | ((uint64_t)cp << 32);
+    sq_emit_any(a, b, cand, C, gm);
   }
+  if (a.mtrace && tid == 0) a.mtrace[(size_t)b * 8 + 4] = ce | ((uint64_t)cp << 32);
   stamp(3);
 }
 

@@ -203,7 +203,7 @@ int bb_get_profile(bb_index* idx, bb_profile* out);
  *                           identical either way.
  *   BB_OPT_SMALL_BATCH      -1 auto (default, = 1), 0 off: batches of up to 16 query rows (any
  *                           mode, hybrid included) on an f32 index of up to 65,536 rows take
- *                           one approximate pass over the bf16 copy per side and an exact
+ *                           one approximate pass over the f16 copy per side and an exact
  *                           rescore of the candidates within its proven bound (no MFMA scan,
  *                           lists or list select) — the reference's one-query request shape.
  *                           Results are identical either way. */
