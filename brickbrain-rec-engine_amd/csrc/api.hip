@@ -188,19 +188,24 @@ struct StreamScope {
 template <typename F>
 int timed(bb_index* x, int fam, hipStream_t s, F&& launch) {
   hipEvent_t a = nullptr, b = nullptr;
-  if (x->prof) {
+  if (x->prof) {  // the family's kernels carry the events themselves (bb_launch, common.h)
     BB_HIP(hipEventCreate(&a));
     BB_HIP(hipEventCreate(&b));
-    BB_HIP(hipEventRecord(a, s));
+    tl_launch_prof = LaunchProf{a, b};
   }
   hipError_t e = launch();
+  const bool none = tl_launch_prof.start != nullptr;  // no kernel went out (a copy, or nothing)
+  tl_launch_prof = LaunchProf{};
   if (e != hipSuccess) {
     if (a) (void)hipEventDestroy(a);
     if (b) (void)hipEventDestroy(b);
     return fail(BB_E_HIP, std::string("launch ") + kFamNames[fam] + ": " + hipGetErrorString(e));
   }
   if (x->prof) {
-    BB_HIP(hipEventRecord(b, s));
+    if (none) {  // a zero-length interval, so the pair still reads
+      BB_HIP(hipEventRecord(a, s));
+      BB_HIP(hipEventRecord(b, s));
+    }
     x->pending.push_back({fam, a, b});
     x->launches[fam] += 1;
   }

@@ -2,6 +2,7 @@
 #pragma once
 #include <cstdlib>
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace bb {
@@ -56,6 +57,27 @@ __device__ __forceinline__ float f16_val(uint16_t h) { return (float)__builtin_b
 // values is off by at most 2^-23 of the largest partial sum, over width/16 chained MFMAs:
 // 17·(width/16)·2^-23 = (17/8)·width·2^-24.
 constexpr double kRrGamma = 17.0 / 8.0 * 0x1p-24;
+
+// Kernel launches.  In a profiled family (api.hip timed()), the launch carries the family's
+// start / stop events itself (hipExtLaunchKernelGGL: the dispatch's own begin / end
+// timestamps, as rocprofv3 reports them — a hipEventRecord pair around the launch adds the
+// dispatch and completion latencies, ~2 us per kernel); the family's first kernel starts the
+// interval and every kernel moves its end.
+struct LaunchProf {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+inline thread_local LaunchProf tl_launch_prof;
+
+template <typename... Args, typename F = void (*)(Args...)>
+inline void bb_launch(F kernel, const dim3& grid, const dim3& block, std::uint32_t shmem, hipStream_t s, Args... args) {
+  LaunchProf& p = tl_launch_prof;
+  if (p.stop) {
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, p.start, p.stop, 0, args...);
+    p.start = nullptr;
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
+  }
+}
 
 // ---- tiling constants ---------------------------------------------------------------------
 constexpr int kTileRows = 128;     // item / query rows are padded to this multiple

@@ -60,26 +60,26 @@ static void launch_scan_t(const GemmArgs& a, hipStream_t s) {
   if constexpr (sizeof(T) == 2 && KU <= kRrMaxD / 8) {
     // the exact re-rank path: the f16 copy of an f32 index (launch_gemm checked a.f16)
     if (a.lists) {  // bounded candidate lists
-      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanList | kScanF16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64),
+      bb_launch((scan2_kernel<T, KU, kScanList | kScanF16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64),
                          0, s, a, n_chunks, tiles);
       return;
     }
     if (a.s_h && !a.cand) {  // int16 score image
-      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanS16 | kScanF16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64),
+      bb_launch((scan2_kernel<T, KU, kScanS16 | kScanF16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64),
                          0, s, a, n_chunks, tiles);
       return;
     }
     if (a.f16) {  // f32 score slab
-      hipLaunchKernelGGL((scan2_kernel<T, KU, kScanF16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
+      bb_launch((scan2_kernel<T, KU, kScanF16>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
                          n_chunks, tiles);
       return;
     }
   }
   if (a.cand)
-    hipLaunchKernelGGL((scan2_kernel<T, KU, kScanStream>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
+    bb_launch((scan2_kernel<T, KU, kScanStream>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
                        n_chunks, tiles);
   else
-    hipLaunchKernelGGL((scan2_kernel<T, KU>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks,
+    bb_launch((scan2_kernel<T, KU>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks,
                        tiles);
 }
 
@@ -115,10 +115,10 @@ static void launch_scan3_t(const GemmArgs& a, hipStream_t s) {
   const int tiles = a.Ncols / 32;
   const int n_chunks = scan_n_chunks(a.Mpad, tiles);
   if (a.cand)
-    hipLaunchKernelGGL((scan3_kernel<KP, kScanStream>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
+    bb_launch((scan3_kernel<KP, kScanStream>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a,
                        n_chunks, tiles);
   else
-    hipLaunchKernelGGL((scan3_kernel<KP>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+    bb_launch((scan3_kernel<KP>), dim3(n_groups * n_chunks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
 }
 
 hipError_t launch_scan3(const GemmArgs& a, hipStream_t s) {
@@ -183,11 +183,11 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   const int blocks = (a.Mpad / bm) * (a.Ncols / bn);
   if (dtype == BF16) {
     constexpr int nt = CfgBF16::WM * CfgBF16::WN * 64;
-    hipLaunchKernelGGL((gemm_nt_kernel<uint16_t, CfgBF16::WM, CfgBF16::WN, CfgBF16::SM, CfgBF16::SN>),
+    bb_launch((gemm_nt_kernel<uint16_t, CfgBF16::WM, CfgBF16::WN, CfgBF16::SM, CfgBF16::SN>),
                        dim3(blocks), dim3(nt), 0, s, a);
   } else {
     constexpr int nt = CfgF32::WM * CfgF32::WN * 64;
-    hipLaunchKernelGGL((gemm_nt_kernel<float, CfgF32::WM, CfgF32::WN, CfgF32::SM, CfgF32::SN>), dim3(blocks),
+    bb_launch((gemm_nt_kernel<float, CfgF32::WM, CfgF32::WN, CfgF32::SM, CfgF32::SN>), dim3(blocks),
                        dim3(nt), 0, s, a);
   }
   return hipGetLastError();

@@ -63,7 +63,7 @@ hipError_t launch_convert_rows(const void* src, int src_dtype, int64_t n, int d,
                                int dst_dtype, int64_t Dpad, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int64_t blocks = (n + 3) / 4;
-  hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, src_dtype, n, d,
+  bb_launch(convert_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, src_dtype, n, d,
                      normalize, dst, dst_dtype, Dpad);
   return hipGetLastError();
 }
@@ -114,7 +114,7 @@ hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t
   if (n % 32 || ld % 8) return hipErrorInvalidValue;  // whole tiles, whole chunks
   const int64_t total = n * (ld >> 3);
   if (total <= 0) return hipSuccess;
-  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, src, n, ld, dst);
+  bb_launch(split_planes_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, src, n, ld, dst);
   return hipGetLastError();
 }
 
@@ -156,7 +156,7 @@ hipError_t launch_rr_prepare(const float* src, int64_t npad, int64_t ld_f, uint1
                              hipStream_t s) {
   if (npad <= 0) return hipSuccess;
   if (ld_b < ld_f) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(rr_prepare_kernel, dim3((unsigned)((npad + 3) / 4)), dim3(256), 0, s, src, npad, ld_f, dst, ld_b,
+  bb_launch(rr_prepare_kernel, dim3((unsigned)((npad + 3) / 4)), dim3(256), 0, s, src, npad, ld_f, dst, ld_b,
                      stats);
   return hipGetLastError();
 }
@@ -300,14 +300,14 @@ __global__ __launch_bounds__(256) void prep2_kernel(PrepArgs a0, PrepArgs a1, in
 
 hipError_t launch_prep(const PrepArgs& a, hipStream_t s) {
   if (a.Bpad <= 0) return hipSuccess;
-  hipLaunchKernelGGL(prep_kernel, dim3((a.Bpad + 3) / 4), dim3(256), 0, s, a);
+  bb_launch(prep_kernel, dim3((a.Bpad + 3) / 4), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_prep2(const PrepArgs& a0, const PrepArgs& a1, hipStream_t s) {
   if (a0.Bpad <= 0 || a1.Bpad <= 0) return hipErrorInvalidValue;
   const int nb0 = (a0.Bpad + 3) / 4, nb1 = (a1.Bpad + 3) / 4;
-  hipLaunchKernelGGL(prep2_kernel, dim3(nb0 + nb1), dim3(256), 0, s, a0, a1, nb0);
+  bb_launch(prep2_kernel, dim3(nb0 + nb1), dim3(256), 0, s, a0, a1, nb0);
   return hipGetLastError();
 }
 
@@ -590,9 +590,9 @@ hipError_t launch_pilot_bound(const uint32_t* top, int n_chunks, int m, int nb, 
   if (!top || !thr_out || n_chunks <= 0 || m <= 0 || 2 * n_chunks * m > 16 * 256 || K <= 0 || B > 32 * nb)
     return hipErrorInvalidValue;
   if (2 * n_chunks * m <= 16 * 64)
-    hipLaunchKernelGGL(pilot_bound_wave_kernel, dim3((B + 3) / 4), dim3(256), 0, s, top, n_chunks, m, nb, K, B, thr_out);
+    bb_launch(pilot_bound_wave_kernel, dim3((B + 3) / 4), dim3(256), 0, s, top, n_chunks, m, nb, K, B, thr_out);
   else
-    hipLaunchKernelGGL(pilot_bound_kernel, dim3(B), dim3(256), 0, s, top, n_chunks, m, nb, K, thr_out);
+    bb_launch(pilot_bound_kernel, dim3(B), dim3(256), 0, s, top, n_chunks, m, nb, K, thr_out);
   return hipGetLastError();
 }
 
@@ -601,9 +601,9 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   if (a.n_rows > a.B || a.P * a.K_int > kFinMerge || a.K_int > kMaxKInt || a.sides < 1 || a.sides > 2) return hipErrorInvalidValue;
   static const bool legacy = ab_env("BB_FINALIZE_LEGACY") != nullptr;
   if (a.P == 1 && !legacy)
-    hipLaunchKernelGGL(finalize1_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
+    bb_launch(finalize1_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
   else
-    hipLaunchKernelGGL(finalize_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
+    bb_launch(finalize_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -634,7 +634,7 @@ __global__ __launch_bounds__(256) void mask_kernel(MaskArgs a) {
 
 hipError_t launch_mask(const MaskArgs& a, hipStream_t s) {
   if (a.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mask_kernel, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+  bb_launch(mask_kernel, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -648,7 +648,7 @@ __global__ void clear_bits_kernel(uint32_t* bits, const int64_t* ids, int64_t n_
 
 hipError_t launch_clear_bits(uint32_t* bits, const int64_t* ids, int64_t n_ids, int64_t n_items, hipStream_t s) {
   if (n_ids <= 0) return hipSuccess;
-  hipLaunchKernelGGL(clear_bits_kernel, dim3((unsigned)((n_ids + 255) / 256)), dim3(256), 0, s, bits, ids, n_ids,
+  bb_launch(clear_bits_kernel, dim3((unsigned)((n_ids + 255) / 256)), dim3(256), 0, s, bits, ids, n_ids,
                      n_items);
   return hipGetLastError();
 }

@@ -32,26 +32,26 @@ static void launch_t(const GemmArgs& a, hipStream_t s) {
   if constexpr (KU <= kRrMaxD / 8) {
     // the exact re-rank path: the f16 copy of an f32 index
     if (a.lists) {  // bounded candidate lists
-      hipLaunchKernelGGL((scan4_kernel<KU, kScanList | kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a,
+      bb_launch((scan4_kernel<KU, kScanList | kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a,
                          n_chunks, tiles);
       return;
     }
     if (a.s_h && !a.cand) {  // int16 score image
-      hipLaunchKernelGGL((scan4_kernel<KU, kScanS16 | kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a,
+      bb_launch((scan4_kernel<KU, kScanS16 | kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a,
                          n_chunks, tiles);
       return;
     }
     if (a.f16) {  // f32 score slab
-      hipLaunchKernelGGL((scan4_kernel<KU, kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+      bb_launch((scan4_kernel<KU, kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
       return;
     }
   }
   if (a.cand)
-    hipLaunchKernelGGL((scan4_kernel<KU, kScanStream>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+    bb_launch((scan4_kernel<KU, kScanStream>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
   else if (a.pilot_top)  // streaming pilot: top-m half-tile maxima, no image
-    hipLaunchKernelGGL((scan4_kernel<KU, kScanPilot>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+    bb_launch((scan4_kernel<KU, kScanPilot>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
   else
-    hipLaunchKernelGGL((scan4_kernel<KU>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
+    bb_launch((scan4_kernel<KU>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
 }
 
 // The hybrid's two re-rank scans (int16 image) in one launch: content rows of 192..512
@@ -62,10 +62,10 @@ static void launch_dual_t(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s)
   const int nc0 = scan4_n_chunks(a0.Mpad, t0), nc1 = scan4_n_chunks(a1.Mpad, t1);
   const int nb0 = a0.Mpad / kScan4Queries * nc0, nb1 = a1.Mpad / kScan4Queries * nc1;
   if (a0.lists)  // bounded candidate lists on both sides (the f16 re-rank copies)
-    hipLaunchKernelGGL((scan4_dual_kernel<KU0, KU1, kScanList | kScanF16>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0,
+    bb_launch((scan4_dual_kernel<KU0, KU1, kScanList | kScanF16>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0,
                        s, a0, a1, nc0, t0, nc1, t1, nb0);
   else
-    hipLaunchKernelGGL((scan4_dual_kernel<KU0, KU1, kScanS16 | kScanF16>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0,
+    bb_launch((scan4_dual_kernel<KU0, KU1, kScanS16 | kScanF16>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0,
                        s, a0, a1, nc0, t0, nc1, t1, nb0);
 }
 template <int KU0>

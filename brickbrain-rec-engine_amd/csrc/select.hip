@@ -1202,9 +1202,9 @@ hipError_t launch_select_rr_wave(const SelectArgs& a, int B, hipStream_t s) {
   static const int um_env = ab_env("BB_WAVE_UM") ? atoi(ab_env("BB_WAVE_UM")) : 0;
   const bool fat = um_env ? um_env == 2 : true;
   if (fat)
-    hipLaunchKernelGGL(select_rr_wave_kernel<2>, dim3(B), dim3(64), 0, s, a);
+    bb_launch(select_rr_wave_kernel<2>, dim3(B), dim3(64), 0, s, a);
   else
-    hipLaunchKernelGGL(select_rr_wave_kernel<1>, dim3(B), dim3(64), 0, s, a);
+    bb_launch(select_rr_wave_kernel<1>, dim3(B), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1217,8 +1217,8 @@ hipError_t launch_select_rr_wave_dual(const SelectArgs& a0, const SelectArgs& a1
         a->n_cols > 64 * kWvTPL * 32 || !a->tmax || (a->max_inout && !a->pmax) || (a->slab_start & 31) ||
         a->out_scores || a->rr_d > 4 * kSelectThreads)
       return hipErrorInvalidValue;
-  hipLaunchKernelGGL(select_rr_wave_dual_kernel, dim3(2 * B), dim3(64), 0, s, a0, a1, B, B);
-  hipLaunchKernelGGL(select_rr_dual_kernel, dim3(2 * B), dim3(kSelectThreads), 0, s, a0, a1, B, B);
+  bb_launch(select_rr_wave_dual_kernel, dim3(2 * B), dim3(64), 0, s, a0, a1, B, B);
+  bb_launch(select_rr_dual_kernel, dim3(2 * B), dim3(kSelectThreads), 0, s, a0, a1, B, B);
   return hipGetLastError();
 }
 
@@ -1226,7 +1226,7 @@ hipError_t launch_rerank(const SelectArgs& a, int B, hipStream_t s) {
   if (!a.rr_eps || !a.rr_x || !a.rr_q || !a.rr_out || !a.rr_cnt || !a.rr_thr || (a.max_inout && (!a.rr_r0 || !a.rr_r0n)) ||
       a.rr_d <= 0 || a.rr_d > kRrMaxD || (a.rr_d & 3) || a.K <= 0 || a.K > kMaxKInt || B <= 0)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(rerank_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
+  bb_launch(rerank_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1234,7 +1234,7 @@ hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s) {
   if (a.K <= 0 || a.K > kMaxKInt || B <= 0 || a.regions <= 0 || a.regions > kCsRegionsMax || a.cap <= 0 ||
       !a.cand || !a.cand_cnt || !a.overflow || (!a.out_scores && !a.keys_out))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(cand_select_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
+  bb_launch(cand_select_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1247,16 +1247,16 @@ hipError_t launch_select(const SelectArgs& a, int B, hipStream_t s) {
                    (a.rr_out && (!a.rr_cnt || !a.rr_thr || (a.max_inout && (!a.rr_r0 || !a.rr_r0n))))))
     return hipErrorInvalidValue;
   if (a.rr_eps) {
-    hipLaunchKernelGGL((select_kernel<0, true>), dim3(B), dim3(kSelectThreads), 0, s, a);
+    bb_launch((select_kernel<0, true>), dim3(B), dim3(kSelectThreads), 0, s, a);
     return hipGetLastError();
   }
   static const int abl = ab_env("BB_SELECT_ABLATE") ? atoi(ab_env("BB_SELECT_ABLATE")) : 0;
   switch (abl) {
-    case 1: hipLaunchKernelGGL(select_kernel<1>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(select_kernel<2>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(select_kernel<4>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
-    case 8: hipLaunchKernelGGL(select_kernel<8>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
-    default: hipLaunchKernelGGL(select_kernel<0>, dim3(B), dim3(kSelectThreads), 0, s, a);
+    case 1: bb_launch(select_kernel<1>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
+    case 2: bb_launch(select_kernel<2>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
+    case 4: bb_launch(select_kernel<4>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
+    case 8: bb_launch(select_kernel<8>, dim3(B), dim3(kSelectThreads), 0, s, a); break;
+    default: bb_launch(select_kernel<0>, dim3(B), dim3(kSelectThreads), 0, s, a);
   }
   return hipGetLastError();
 }

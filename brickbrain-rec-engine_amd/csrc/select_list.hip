@@ -566,9 +566,9 @@ static bool list_args_ok(const SelectArgs& a) {
 hipError_t launch_select_list(const SelectArgs& a0, const SelectArgs* a1, int B, hipStream_t s) {
   if (B <= 0 || !list_args_ok(a0) || (a1 && !list_args_ok(*a1))) return hipErrorInvalidValue;
   if (a1)
-    hipLaunchKernelGGL(select_list_dual_kernel, dim3(2 * B), dim3(kSelectThreads), 0, s, a0, *a1, B);
+    bb_launch(select_list_dual_kernel, dim3(2 * B), dim3(kSelectThreads), 0, s, a0, *a1, B);
   else
-    hipLaunchKernelGGL(select_list_kernel, dim3(B), dim3(kSelectThreads), 0, s, a0, B);
+    bb_launch(select_list_kernel, dim3(B), dim3(kSelectThreads), 0, s, a0, B);
   return hipGetLastError();
 }
 

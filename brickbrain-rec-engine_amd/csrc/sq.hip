@@ -684,7 +684,7 @@ __global__ __launch_bounds__(kSqThreads) void sq_merge_kernel(SqArgs a0, SqArgs 
 template <int KS>
 hipError_t launch_sq_ks(const SqArgs& a, hipStream_t s) {
   const size_t lds = (size_t)a.B * a.ldx * 4 + (size_t)a.B * a.rpw * 4;  // <= 40 KiB
-  hipLaunchKernelGGL(sq_scan_kernel<KS>, dim3(a.nwg), dim3(kSqThreads), lds, s, a);
+  bb_launch(sq_scan_kernel<KS>, dim3(a.nwg), dim3(kSqThreads), lds, s, a);
   return hipGetLastError();
 }
 
@@ -715,7 +715,7 @@ hipError_t launch_sq_merge(const SqArgs& a0, const SqArgs* a1, hipStream_t s) {
       (a0.out_scores ? (!a0.out_ids || a0.k_final < 1 || a0.k_final > a0.K) : !a0.keys_out) ||
       (a1 && !a1->keys_out))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(sq_merge_kernel, dim3(a1 ? 2 * a0.B : a0.B), dim3(kSqThreads), 0, s, a0, a1 ? *a1 : a0);
+  bb_launch(sq_merge_kernel, dim3(a1 ? 2 * a0.B : a0.B), dim3(kSqThreads), 0, s, a0, a1 ? *a1 : a0);
   return hipGetLastError();
 }
 
