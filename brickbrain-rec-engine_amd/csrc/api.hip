@@ -834,12 +834,12 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       BB_HIP(hipMemcpyAsync(tr.data(), x->trace.p, tr.size() * 8, hipMemcpyDeviceToHost, s));
       BB_HIP(hipStreamSynchronize(s));
       uint64_t t0 = ~0ull, tend = 0;
-      double ph[5] = {0};
+      double ph[6] = {0};
       for (int w2 = 0; w2 < nwg; ++w2) {
         const uint64_t* t = &tr[(size_t)w2 * 8];
         t0 = std::min(t0, t[0]);
         tend = std::max(tend, t[4]);
-        for (int j = 1; j < 5; ++j) ph[j] += (double)(t[j] - t[0]);
+        for (int j = 1; j < 6; ++j) ph[j] += t[j] ? (double)(t[j] - t[0]) : 0.0;
       }
       uint64_t s_max = 0;
       for (int w2 = 0; w2 < nwg; ++w2) s_max = std::max<uint64_t>(s_max, tr[(size_t)w2 * 8] - t0);
@@ -853,10 +853,11 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         ce += (double)(uint32_t)t[4];
         cp += (double)(t[4] >> 32);
       }
-      fprintf(stderr, "[bb sq trace] B=%d nwg=%d rpw=%d pass (us from workgroup start): loads-issued %.2f q-ready %.2f "
-              "rows-done %.2f end %.2f | starts spread %.2f, span %.2f | merge: gathered %.2f rescored %.2f end %.2f, "
-              "span %.2f, cands %.1f + r0 %.1f | pass end -> merge start %.2f\n",
-              B, nwg, rpw, ph[1] / nwg / 100, ph[2] / nwg / 100, ph[3] / nwg / 100, ph[4] / nwg / 100, (double)s_max / 100,
+      fprintf(stderr, "[bb sq trace] B=%d nwg=%d rpw=%d pass (us from workgroup start): queries-loaded %.2f "
+              "queries-normalised %.2f mfma-done %.2f order-images %.2f end %.2f | starts spread %.2f, span %.2f | merge: "
+              "gathered %.2f rescored %.2f end %.2f, span %.2f, cands %.1f + r0 %.1f | pass end -> merge start %.2f\n",
+              B, nwg, rpw, ph[1] / nwg / 100, ph[2] / nwg / 100, ph[3] / nwg / 100, ph[5] / nwg / 100, ph[4] / nwg / 100,
+              (double)s_max / 100,
               (double)(tend - t0) / 100, mp[1] / B / 100, mp[2] / B / 100, mp[3] / B / 100, (double)(m1 - m0) / 100, ce / B,
               cp / B, ((double)m0 - (double)tend) / 100);
     }

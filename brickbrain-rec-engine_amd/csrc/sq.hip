@@ -408,6 +408,7 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
         }
       }
     }
+    stamp(5);
     for (int set = 0; set < (a.drop ? 2 : 1); ++set) {  // wave-uniform
       uint64_t mine[NQ];
 #pragma unroll

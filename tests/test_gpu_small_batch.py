@@ -164,6 +164,32 @@ def test_cf_rated_excluded(brickrec):
         idx.close()
 
 
+def test_f16_range_saturation(brickrec):
+    """Values beyond the f16 range (|x| > 65504) saturate in the approximate copy and in the
+    query operands; every bound is computed from the saturated values, so those rows and
+    queries only widen the candidate window (here: into the exact slow paths) — both paths
+    stay exact.  CF factors with a few huge entries, and one user row with a huge entry."""
+    n, r, B = 25216, 50, 4
+    rng = np.random.default_rng(12)
+    x = R.unit_rows(n, 384, 6)
+    f = rng.normal(0, 0.1, (n, r)).astype(np.float32)
+    hot = rng.choice(n, 40, replace=False)
+    f[hot, rng.integers(0, r, 40)] = rng.choice([-1.0, 1.0], 40) * 2.0e5
+    u = rng.normal(0, 0.1, (B, r)).astype(np.float32)
+    u[1, 7] = 1.5e5
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x, prenormalized=True)
+        idx.upload_cf(f)
+        sc, ids, cnt = _all_variants(idx, "cf", 20, q_cf=u)
+        for b in range(B):
+            ri, rs = _exact(f, u[b], 20, np.ones(n, bool))
+            assert list(ids[b]) == list(ri)
+            assert np.array_equal(sc[b].view(np.uint32), rs.view(np.uint32))
+    finally:
+        idx.close()
+
+
 @pytest.mark.parametrize("B", [1, 3, 16])
 def test_hybrid_requests(brickrec, B):
     """HybridRecommender.get_recommendations' shape (recommendation_system.py:612-677): liked set
