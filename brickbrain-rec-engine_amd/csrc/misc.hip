@@ -247,11 +247,12 @@ __device__ __forceinline__ void prep_rows(const PrepArgs& a, int blk) {
     double x[kPrepC];
     load_chunk<kPrepC>(src, sdt, sb, 0, d, lane, x);
     const double norm = norm_on ? qn_norm(x) : 1.0;  // (qnorm.h: the list select's raw path shares it)
+    const double rinv = 1.0 / norm;
 #pragma unroll
     for (int c = 0; c < kPrepC; ++c) {
       const int i = lane + 64 * c;
       if (i < a.Dpad) {
-        const float v = qn_elem(x[c], norm);
+        const float v = qn_elem(x[c], norm, rinv);
         store_q(a, row, i, v);
         if (a.out_f32) rr.add(a, row, i, v);
       }
@@ -279,7 +280,7 @@ __device__ __forceinline__ void prep_rows(const PrepArgs& a, int blk) {
     for (int c = 0; c < kPrepC; ++c) {
       const int i = base + lane + 64 * c;
       if (i < a.Dpad) {
-        const float v = (float)(x[c] / norm);
+        const float v = qn_elem(x[c], norm, 1.0 / norm);
         store_q(a, row, i, v);
         if (a.out_f32) rr.add(a, row, i, v);
       }

@@ -30,7 +30,17 @@ __device__ __forceinline__ double qn_norm(const double (&x)[kQnC]) {
   return nrm == 0.0 ? 1.0 : nrm;
 }
 
-__device__ __forceinline__ float qn_elem(double x, double nrm) { return (float)(x / nrm); }
+// (float)(x / nrm) — the f64 quotient rounded to f32 — from rinv = 1 / nrm (one division per
+// row): q = x·rinv is within 2^-51.9 (relative) of x / nrm and of its correctly rounded f64
+// quotient; when q·(1 ∓ 2^-50) round to the same f32, so does that quotient (f32 rounding is
+// monotonic), and only a q within that distance of an f32 rounding boundary (a fraction
+// ~2^-27 of elements) divides.  The same bits as the division, for ~1/10 of its dependent f64
+// latency per element.
+__device__ __forceinline__ float qn_elem(double x, double nrm, double rinv) {
+  const double q = x * rinv, e = fabs(q) * 0x1p-50;
+  const float lo = (float)(q - e), hi = (float)(q + e);
+  return lo == hi ? lo : (float)(x / nrm);
+}
 
 // Load C elements per lane (i = base + lane + 64c, zero past `d`) with the dtype switch
 // outside the loads, so all C loads are in flight together: every load is unconditional (the

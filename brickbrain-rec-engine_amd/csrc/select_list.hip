@@ -336,11 +336,11 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     double xd[kQnC];
 #pragma unroll
     for (int c = 0; c < kQnC; ++c) xd[c] = (double)xq[c];
-    const double nrm = qn_norm(xd);
+    const double nrm = qn_norm(xd), rinv = 1.0 / nrm;
 #pragma unroll
     for (int c = 0; c < kQnC; ++c) {
       const int i = lane + 64 * c;
-      if (i < a.rr_d) qs[i] = qn_elem(xd[c], nrm);
+      if (i < a.rr_d) qs[i] = qn_elem(xd[c], nrm, rinv);
     }
   }
   __syncthreads();

@@ -303,8 +303,10 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
 #pragma unroll
       for (int t = 0; t < NQ; ++t) nrm[t] = 1.0;
     }
-    double ss[NQ];
+    double ss[NQ], rinv[NQ];
     float mx[NQ];
+#pragma unroll
+    for (int t = 0; t < NQ; ++t) rinv[t] = 1.0 / nrm[t];
 #pragma unroll
     for (int t = 0; t < NQ; ++t) {
       const int b = w + kSqWaves * t;
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
       for (int c = 0; c < kQnC; ++c) {
         const int i = lane + 64 * c;
         if (i < ldx) {
-          const float v = qn_elem(xq[t][c], nrm[t]);
+          const float v = qn_elem(xq[t][c], nrm[t], rinv[t]);
           qs[b * ldx + i] = v;
           if (blk == 0) {
             a.q_out[(size_t)b * ldx + i] = v;
