@@ -125,7 +125,7 @@ struct bb_index {
   DevBuf rr_flags;     // one-wave re-rank select: rows left to the block select
   DevBuf list1, max1;  // two-level streaming: exact top-K_int (+ rank-0 key) of items [0, n1)
   DevBuf lists, r0lists;  // bounded candidate lists of the list scans (list_epi.h), both sides
-  DevBuf sq_top, sq_ptop, sq_ords, sq_q;  // small-batch exact search (sq.hip)
+  DevBuf sq_top, sq_ptop, sq_ords;  // small-batch exact search (sq.hip)
   uint32_t* ovf_host = nullptr;  // pinned
 
   bool prof = false;
@@ -365,7 +365,7 @@ int bb_destroy(bb_index* x) {
                       &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
                       &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
                       &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists, &x->pilot_top,
-                      &x->sq_top, &x->sq_ptop, &x->sq_ords, &x->sq_q})
+                      &x->sq_top, &x->sq_ptop, &x->sq_ords})
       b->release();
     if (x->ovf_host) (void)hipHostFree(x->ovf_host);
     if (x->has_last) (void)hipEventSynchronize(x->done);
@@ -753,9 +753,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     const int32_t rpw = (int32_t)std::min<int64_t>(kSqMaxRows, std::max<int64_t>(4, round_up((x->n + wg_goal - 1) / wg_goal, 4)));
     const int32_t nwg = (int32_t)((x->n + rpw - 1) / rpw);
     const size_t top_side = (size_t)B * nwg * kSqM, ord_side = (size_t)B * x->n * 2;
-    const size_t q_side = (size_t)B * kRrMaxD;
     if ((rc = x->sq_top.ensure(top_side * 8 * sides)) || (rc = x->sq_ptop.ensure(top_side * 8)) ||
-        (rc = x->sq_ords.ensure(ord_side * 4 * sides)) || (rc = x->sq_q.ensure((q_side + B) * 4 * sides)) ||
+        (rc = x->sq_ords.ensure(ord_side * 4 * sides)) ||
         (rc = x->keys.ensure((size_t)sides * B * K_int * 8)) || (rc = x->maxk.ensure((size_t)B * 8)))
       return rc;
     const bool host_res = !out_keys && res->where != BB_DEVICE;
@@ -794,8 +793,6 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         a.q_ids = (const int64_t*)d_items;
         a.q_id_offset = x->id_offset;
       }
-      a.q_out = (float*)x->sq_q.p + side * q_side;
-      a.q_margin = (float*)x->sq_q.p + sides * q_side + side * B;
       a.rpw = rpw;
       a.nwg = nwg;
       a.K = K_int;

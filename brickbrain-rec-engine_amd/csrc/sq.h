@@ -34,7 +34,8 @@ struct SqArgs {
   int64_t excl_ld;
   int32_t drop;             // rank-0 drop: keep the present candidates too
   int32_t B;
-  // queries: q_kind 0 = raw rows q_src (q_dtype, stride q_ld, width q_d) normalised as
+  // queries: q_kind 0 = raw rows q_src (q_dtype, stride q_ld, width q_d): the pass scores
+  // them as given (times a power-of-two scale), the merge rescores them normalised as
   // prep_kernel does (qnorm.h); 1 = the stored f32 rows of ids q_ids (minus q_id_offset) of X;
   // 2 = q_src rows as they are (CF user factors)
   int32_t q_kind;
@@ -44,8 +45,6 @@ struct SqArgs {
   int32_t q_d;
   const int64_t* q_ids;
   int64_t q_id_offset;
-  float* q_out;             // [B][ldx] the f32 query rows (written by workgroup 0) for the rescore
-  float* q_margin;          // [B] their re-rank margins 2δ (written by workgroup 0)
   int32_t rpw, nwg;         // rows per workgroup (multiple of 4), workgroups
   uint64_t* wg_top;         // [B][nwg][kSqM] eligible approximate keys (0 = empty)
   uint64_t* wg_ptop;        // [B][nwg][kSqM] present approximate keys (drop)

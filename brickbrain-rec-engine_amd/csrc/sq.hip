@@ -176,7 +176,10 @@ __device__ __forceinline__ void split_f16x8(const float (&v)[8], u4v& hi, u4v& l
 // accumulation of the 2·ldb exact f16 products, Σ|x̃_j|(|h_j| + |l_j|) <= Ñ_x(‖h‖ + ‖l‖), over
 // 2·ldb/32 chained MFMAs of 32 products + the accumulator each, every one of the 33 values
 // rounded or truncated by at most 2^-23 of the largest partial sum whatever the matrix core's
-// order (γ = 33·(2·ldb/32)·2^-23); and the f32 rounding of s (2^-23·N_x).  Toward-zero f16
+// order (γ = 33·(2·ldb/32)·2^-23); and, the pass scoring the row as given (times its scale c)
+// where the exact score s uses prep's normalised f32 row, |c·s − x·q| <= 2^-22·N_x·‖q‖ (the
+// f32 rounding of every normalised element, of the raw f64 / bf16 input, and of s itself, in
+// the units of the scaled row).  Toward-zero f16
 // rounding is off by < 2^-10·|v| + 2^-24 (the subnormal spacing), so
 //   ‖h‖ <= ‖q‖,  ‖l‖ <= ‖q − h‖ <= 2^-10·‖q‖ + 2^-24·√ldx,  ‖r‖ <= 2^-20·‖q‖ + 2^-23·√ldx.
 // A row reaching the f16 range (|q_j| >= 2^15) gets an infinite margin: every item is then a
@@ -187,8 +190,84 @@ __device__ __forceinline__ float sq_margin_of(const SqArgs& a, double qn, float 
   const double hl = qn * (1.0 + 0x1p-10) + 0x1p-24 * rt, rn = 0x1p-20 * qn + 0x1p-23 * rt;
   const double gam = 33.0 * (2.0 * (double)a.ldb / 32.0) * 0x1p-23;
   const double ex = (double)a.stats[0], nx = (double)a.stats[1], nxb = (double)a.stats[2];
-  const double d = ex * qn + nxb * rn + gam * nxb * hl + 0x1p-23 * nx * qn;
+  const double d = ex * qn + nxb * rn + gam * nxb * hl + 0x1p-22 * nx * qn;
   return rr_margin(__double2float_ru(d * (1.0 + 0x1p-20)));
+}
+
+// the margin of one query row as the pass scored it (v: the row before its scale; the whole
+// wave): ‖c·q‖ and max |c·q| of the scaled row, then sq_margin_of
+__device__ __forceinline__ float sq_margin_row(const SqArgs& a, const float (&v)[kQnC]);
+
+// The query rows of a wave as the pass and the merge see them: element lane + 64c of row
+// b = min(w0 + step·t, B − 1) of the query source, as f32 — raw rows (q_kind 0, rounded to
+// f32 when given as f64 / bf16) or CF rows (2) as they are, the stored f32 rows of item ids
+// (1); zero past the row.  All loads are issued before any is used; `then` runs between the
+// issue and the first use (the pass issues its item rows there).
+template <int QT, typename Then>
+__device__ __forceinline__ void sq_query_rows(const SqArgs& a, int w0, int step, int lane, float (&qv)[QT][kQnC],
+                                              Then&& then) {
+  const int B = a.B, ldx = (int)a.ldx;
+  if (a.q_kind != 1 && a.q_dtype != F32) {  // (uniform) bf16 / f64 rows: the generic loader
+    double xq[QT][kQnC];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+      load_chunk<kQnC>(a.q_src, a.q_dtype, (size_t)min(w0 + step * t, B - 1) * a.q_ld, 0, a.q_d, lane, xq[t]);
+    then();
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int c = 0; c < kQnC; ++c) qv[t][c] = (float)xq[t][c];
+    return;
+  }
+  int64_t qid[QT];
+  if (a.q_kind == 1) {
+#pragma unroll
+    for (int t = 0; t < QT; ++t) qid[t] = a.q_ids[min(w0 + step * t, B - 1)] - a.q_id_offset;
+  }
+  bool qok[QT];
+  const int qlen = a.q_kind == 1 ? ldx : a.q_d;
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int b = min(w0 + step * t, B - 1);
+    qok[t] = a.q_kind != 1 || (qid[t] >= 0 && qid[t] < a.n);
+    const float* src = a.q_kind == 1 ? a.X + (size_t)(qok[t] ? qid[t] : 0) * ldx : (const float*)a.q_src + (size_t)b * a.q_ld;
+#pragma unroll
+    for (int c = 0; c < kQnC; ++c) qv[t][c] = src[min(lane + 64 * c, qlen - 1)];
+  }
+  then();
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+#pragma unroll
+    for (int c = 0; c < kQnC; ++c) qv[t][c] = qok[t] && lane + 64 * c < qlen ? qv[t][c] : 0.f;
+}
+
+// The power-of-two scale 2^k of a query row (the wave's lanes: elements lane + 64c) that puts
+// its largest element in [2^13, 2^14): exact, so the scaled row is the row times a positive
+// constant, and well inside the f16 range of the split (an all-zero or non-finite row: 1).
+__device__ __forceinline__ float sq_row_scale(const float (&v)[kQnC]) {
+  float m = 0.f;
+#pragma unroll
+  for (int c = 0; c < kQnC; ++c) m = fmaxf(m, fabsf(v[c]));
+  m = __int_as_float((int)wave_max_u32((uint32_t)__float_as_int(m)));  // non-negative: bits order
+  if (!(m > 0.f) || !(m <= 3.4e38f)) return 1.f;
+  int e;
+  (void)frexpf(m, &e);  // m = f·2^e, f in [0.5, 1)
+  return ldexpf(1.f, 14 - e);
+}
+
+__device__ __forceinline__ float sq_margin_row(const SqArgs& a, const float (&v)[kQnC]) {
+  const float sc = sq_row_scale(v);
+  double ss = 0.0;
+  float mx = 0.f;
+#pragma unroll
+  for (int c = 0; c < kQnC; ++c) {
+    const float x = v[c] * sc;
+    ss = fma((double)x, (double)x, ss);
+    mx = fmaxf(mx, fabsf(x));
+  }
+  ss = qn_wave_sum(ss);
+  mx = __int_as_float((int)wave_max_u32((uint32_t)__float_as_int(mx)));
+  return sq_margin_of(a, sqrt(ss) * (1.0 + 0x1p-40), mx);
 }
 
 // Approximate pass on the matrix cores.  Each wave scores whole 16-row chunks of the
@@ -212,13 +291,14 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
     if (a.trace && tid == 0) a.trace[(size_t)blk * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  // query rows, as prep_kernel writes its f32 operand: normalised raw rows (qnorm.h), the
-  // stored rows of item ids, or CF rows as they are; zero past the row.  Every query load of
-  // the wave (rows b = w, w + 4, ...) is issued before any is used, then this wave's chunks of
-  // item rows — unconditionally (a chunk past the block reloads row r0), so that the first use
-  // of a query element waits for the query loads only and leaves the chunks in flight (a branch
-  // between them would make the compiler drain everything).  Workgroup 0 also hands the rows
-  // to the merge (q_out) with their margins (q_margin).
+  // query rows as the pass scores them (sq_query_row): raw rows as given (rounded to f32), the
+  // stored rows of item ids, CF rows — each times its power-of-two scale (sq_row_scale), so the
+  // approximate scores are a positive multiple of the exact ones and no workgroup normalises
+  // (the merge does, once per query, for the rescore).  Every query load of the wave (rows
+  // b = w, w + 4, ...) is issued before any is used, then this wave's chunks of item rows —
+  // unconditionally (a chunk past the block reloads row r0), so that the first use of a query
+  // element waits for the query loads only and leaves the chunks in flight (a branch between
+  // them would make the compiler drain everything).
   constexpr int QT = kSqMaxB / kSqWaves;
   constexpr int NCW = kSqMaxRows / 16 / kSqWaves;  // chunks per wave
   u4v af[NCW][KS];
@@ -245,104 +325,31 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
     }
     asm volatile("" ::: "memory");  // the scheduler would sink these loads below the query's first use
   };
-  double xq[QT][kQnC];
-  if (a.q_kind != 1 && a.q_dtype != F32) {  // (uniform) bf16 / f64 query rows: the generic loader
-#pragma unroll
-    for (int t = 0; t < QT; ++t)
-      load_chunk<kQnC>(a.q_src, a.q_dtype, (size_t)min(w + kSqWaves * t, B - 1) * a.q_ld, 0, a.q_d, lane, xq[t]);
-    load_rows();
-  } else {
-    int64_t qid[QT];
-    if (a.q_kind == 1) {
-#pragma unroll
-      for (int t = 0; t < QT; ++t) qid[t] = a.q_ids[min(w + kSqWaves * t, B - 1)] - a.q_id_offset;
-    }
-    float qv[QT][kQnC];
-    bool qok[QT];
-    const int qlen = a.q_kind == 1 ? ldx : a.q_d;
-#pragma unroll
-    for (int t = 0; t < QT; ++t) {
-      const int b = min(w + kSqWaves * t, B - 1);
-      qok[t] = a.q_kind != 1 || (qid[t] >= 0 && qid[t] < a.n);
-      const float* src = a.q_kind == 1 ? a.X + (size_t)(qok[t] ? qid[t] : 0) * ldx
-                                       : (const float*)a.q_src + (size_t)b * a.q_ld;
-#pragma unroll
-      for (int c = 0; c < kQnC; ++c) qv[t][c] = src[min(lane + 64 * c, qlen - 1)];
-    }
-    load_rows();
-#pragma unroll
-    for (int t = 0; t < QT; ++t)
-#pragma unroll
-      for (int c = 0; c < kQnC; ++c) xq[t][c] = qok[t] && lane + 64 * c < qlen ? (double)qv[t][c] : 0.0;
-  }
+  float qv[QT][kQnC];
+  sq_query_rows<QT>(a, w, kSqWaves, lane, qv, load_rows);
   stamp(1);
-  // this wave's queries (b = w + 4t, t < nq): norms with their butterflies interleaved across
-  // the rows (per row the operations and order of qn_norm: the same bits), then the f32 rows
+  // this wave's queries (b = w + 4t, t < nq): scaled into LDS, the rows' maxima interleaved
   const int nq = B > w ? (B - w + kSqWaves - 1) / kSqWaves : 0;  // (wave-uniform)
-  auto norm_rows = [&](auto NQC) __attribute__((always_inline)) {
+  auto scale_rows = [&](auto NQC) __attribute__((always_inline)) {
     constexpr int NQ = decltype(NQC)::value;
-    double nrm[NQ];
-    if (a.q_kind == 0) {
-      double s2[NQ];
+    float sc[NQ];
 #pragma unroll
-      for (int t = 0; t < NQ; ++t) {
-        s2[t] = 0.0;
-#pragma unroll
-        for (int c = 0; c < kQnC; ++c) s2[t] = fma(xq[t][c], xq[t][c], s2[t]);
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-        for (int t = 0; t < NQ; ++t) s2[t] += __shfl_xor(s2[t], o);
-#pragma unroll
-      for (int t = 0; t < NQ; ++t) {
-        const double r = sqrt(s2[t]);
-        nrm[t] = r == 0.0 ? 1.0 : r;
-      }
-    } else {
-#pragma unroll
-      for (int t = 0; t < NQ; ++t) nrm[t] = 1.0;
-    }
-    double ss[NQ], rinv[NQ];
-    float mx[NQ];
-#pragma unroll
-    for (int t = 0; t < NQ; ++t) rinv[t] = 1.0 / nrm[t];
+    for (int t = 0; t < NQ; ++t) sc[t] = sq_row_scale(qv[t]);
 #pragma unroll
     for (int t = 0; t < NQ; ++t) {
       const int b = w + kSqWaves * t;
-      ss[t] = 0.0;
-      mx[t] = 0.f;
 #pragma unroll
       for (int c = 0; c < kQnC; ++c) {
         const int i = lane + 64 * c;
-        if (i < ldx) {
-          const float v = qn_elem(xq[t][c], nrm[t], rinv[t]);
-          qs[b * ldx + i] = v;
-          if (blk == 0) {
-            a.q_out[(size_t)b * ldx + i] = v;
-            ss[t] = fma((double)v, (double)v, ss[t]);
-            mx[t] = fmaxf(mx[t], fabsf(v));
-          }
-        }
-      }
-    }
-    if (blk == 0) {  // (workgroup-uniform) the margins
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-        for (int t = 0; t < NQ; ++t) ss[t] += __shfl_xor(ss[t], o);
-#pragma unroll
-      for (int t = 0; t < NQ; ++t) {
-        const float m = __int_as_float((int)wave_max_u32((uint32_t)__float_as_int(mx[t])));  // non-negative: bits order
-        if (lane == 0) a.q_margin[w + kSqWaves * t] = sq_margin_of(a, sqrt(ss[t]) * (1.0 + 0x1p-40), m);
+        if (i < ldx) qs[b * ldx + i] = qv[t][c] * sc[t];
       }
     }
   };
   switch (nq) {
-    case 1: norm_rows(std::integral_constant<int, 1>{}); break;
-    case 2: norm_rows(std::integral_constant<int, 2>{}); break;
-    case 3: norm_rows(std::integral_constant<int, 3>{}); break;
-    case 4: norm_rows(std::integral_constant<int, 4>{}); break;
+    case 1: scale_rows(std::integral_constant<int, 1>{}); break;
+    case 2: scale_rows(std::integral_constant<int, 2>{}); break;
+    case 3: scale_rows(std::integral_constant<int, 3>{}); break;
+    case 4: scale_rows(std::integral_constant<int, 4>{}); break;
     default: break;
   }
   __syncthreads();
@@ -467,7 +474,8 @@ __global__ __launch_bounds__(kSqThreads) void sq_scan_kernel(SqArgs a) {
 // workgroup whose kSqM-th key reaches it that its list did not hold.  Returns the count (it
 // may exceed cap: the caller's slow path) and the bound.
 template <int NL>  // nwg <= 64·NL
-__device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint32_t* ords, int K, const float* mp,
+__device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* tops, const uint32_t* ords, int K,
+                                              const float (&qv)[kQnC],
                               bool kth, uint64_t* cb, uint32_t cap, uint32_t* T_out) {
   const int lane = threadIdx.x & 63;
   const int nwg = a.nwg;
@@ -478,7 +486,7 @@ __device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* t
 #pragma unroll
     for (int j = 0; j < kSqM; ++j) ent[i][j] = t < nwg ? tops[(size_t)t * kSqM + j] : 0ull;
   }
-  const float margin = *mp;
+  const float margin = sq_margin_row(a, qv);
   uint32_t top;
   if (kth) {  // the largest multiple of 2^16 with >= K workgroup maxima at or above it
     uint32_t prefix = 0;
@@ -615,27 +623,48 @@ __device__ __forceinline__ void sq_merge_row(const SqArgs& a, int b, SqMergeLds&
   uint32_t* misc = L.misc;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int ldx = (int)a.ldx;
-  const float* qrow = a.q_out + (size_t)b * ldx;
-  const float* mp = a.q_margin + b;
   auto stamp = [&](int slot) {  // BB_SQ_TRACE probe runs: phase timeline (100 MHz)
     if (a.mtrace && tid == 0) a.mtrace[(size_t)b * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  for (int i = tid; i < ldx; i += kSqThreads) qs[i] = qrow[i];
+  // every wave: the query row as the pass scored it (before its scale); wave 2 writes the
+  // rescore's f32 row into LDS — normalised with prep's arithmetic (qnorm.h: the same bits as
+  // every other path) for raw rows, as it is otherwise — while waves 0 and 1 gather
+  float qv[1][kQnC];
+  sq_query_rows<1>(a, b, 0, lane, qv, [] {});
+  if (w == 2) {
+    if (a.q_kind == 0) {
+      double x[kQnC];
+      if (a.q_dtype == F32) {
+#pragma unroll
+        for (int c = 0; c < kQnC; ++c) x[c] = (double)qv[0][c];
+      } else {
+        load_chunk<kQnC>(a.q_src, a.q_dtype, (size_t)b * a.q_ld, 0, a.q_d, lane, x);
+      }
+      const double nrm = qn_norm(x), rinv = 1.0 / nrm;
+#pragma unroll
+      for (int c = 0; c < kQnC; ++c)
+        if (lane + 64 * c < ldx) qs[lane + 64 * c] = qn_elem(x[c], nrm, rinv);
+    } else {
+#pragma unroll
+      for (int c = 0; c < kQnC; ++c)
+        if (lane + 64 * c < ldx) qs[lane + 64 * c] = qv[0][c];
+    }
+  }
   if (w == 0) {
     uint32_t T;
     const uint64_t* tops = a.wg_top + (size_t)b * a.nwg * kSqM;
     const uint32_t* ords = a.ords + (size_t)b * a.ords_ld;
-    const uint32_t ce = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, a.K, mp, true, cand, kSqCand, &T)
-                                                      : sq_gather<8>(a, tops, ords, a.K, mp, true, cand, kSqCand, &T);
+    const uint32_t ce = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, a.K, qv[0], true, cand, kSqCand, &T)
+                                                      : sq_gather<8>(a, tops, ords, a.K, qv[0], true, cand, kSqCand, &T);
     if (lane == 0) misc[0] = ce, misc[2] = T;
   } else if (w == 1) {
     uint32_t T = 0xFFFFFFFFu, cp = 0;
     if (a.drop) {
       const uint64_t* tops = a.wg_ptop + (size_t)b * a.nwg * kSqM;
       const uint32_t* ords = a.ords_p + (size_t)b * a.ords_ld;
-      cp = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, 1, mp, false, ptmp, kSqPCand, &T)
-                                        : sq_gather<8>(a, tops, ords, 1, mp, false, ptmp, kSqPCand, &T);
+      cp = (a.mopt & 1) && a.nwg <= 256 ? sq_gather<4>(a, tops, ords, 1, qv[0], false, ptmp, kSqPCand, &T)
+                                        : sq_gather<8>(a, tops, ords, 1, qv[0], false, ptmp, kSqPCand, &T);
     }
     if (lane == 0) misc[1] = cp, misc[3] = T;
   }
@@ -697,8 +726,8 @@ hipError_t launch_sq_scan(const SqArgs& a, hipStream_t s) {
   if (a.B < 1 || a.B > kSqMaxB || a.ldx > kRrMaxD || (a.ldx & 31) || a.ldb < a.ldx || (a.ldb & 63) || a.ldb > 512 ||
       a.K < 1 || a.K > kSqMaxK || a.rpw < 4 || (a.rpw & 3) || a.rpw > kSqMaxRows || a.nwg < 1 || a.nwg > kSqMaxWg ||
       (int64_t)a.nwg * a.rpw < a.n || (int64_t)(a.nwg - 1) * a.rpw >= a.n || a.n < 1 || a.ords_ld < a.n ||
-      !a.present || !a.mask || !a.excl || a.excl_ld < 0 || !a.Xb || !a.X || !a.stats || !a.q_out || !a.q_margin ||
-      (a.drop && (!a.ords_p || !a.wg_ptop)))
+      !a.present || !a.mask || !a.excl || a.excl_ld < 0 || !a.Xb || !a.X || !a.stats ||
+      (a.q_kind == 1 ? !a.q_ids : !a.q_src) || (a.drop && (!a.ords_p || !a.wg_ptop)))
     return hipErrorInvalidValue;
   switch (a.ldb / 32) {
     case 2: return launch_sq_ks<2>(a, s);
