@@ -670,9 +670,14 @@ def main():
         alg_bytes = N_ITEMS * (DIM + r) * es + B * (r * 4 + 8) + B * TOPK * 12 + N_ITEMS // 8
         kname, mpf = scan_kernel_info(args.dtype, DIM, B)
         ab = os.environ.get("BB_AB")
-        if args.dtype == "f32" and not (ab and os.environ.get("BB_NO_RR")) and not (ab and os.environ.get("BB_DUAL") == "0"):
-            kname = ("scan4_dual_kernel<48,8,list|f16> (content d=384 + CF r=50 one-product f16 scans in one launch, "
-                     "bounded per-lane candidate lists; exact f32 re-rank of the candidates in the list select)")
+        if args.dtype == "f32" and not (ab and os.environ.get("BB_NO_RR")):
+            if ab and os.environ.get("BB_DUAL") == "1":
+                kname = ("scan4_dual_kernel<48,8,list|f16> (content d=384 + CF r=50 one-product f16 scans in one "
+                         "launch, bounded per-lane candidate lists; exact f32 re-rank of the candidates in the list select)")
+            else:
+                kname = ("scan4_kernel<48,list|f16> + scan4_kernel<8,list|f16> (content d=384 and CF r=50 one-product "
+                         "f16 scans, one launch per side, the CF side at twice the chunks; bounded per-lane candidate "
+                         "lists; exact f32 re-rank of the candidates in the list select)")
     else:
         flops = 2.0 * B * N_ITEMS * DIM
         alg_bytes = N_ITEMS * DIM * es + B * DIM * 4 + B * TOPK * 8    # items + queries + top-K out

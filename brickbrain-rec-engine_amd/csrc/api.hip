@@ -699,10 +699,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   // chunk of bpad_c rows: item chunks of the scan launch (scan2 or scan4), periods per chunk
   // (enough lists that a list expects <= 1/3 of a top-K member: 2·chunks·periods >= 3·K_int),
   // tiles per period.
-  auto list_geom = [&](int bpad_c, int& nch, int& np, int& G) -> bool {
+  auto list_geom = [&](int bpad_c, int ku, int& nch, int& np, int& G) -> bool {
     if (x->lists_opt == 0) return false;
     const int tiles = (int)(round_up(x->n, kTileRows) / 32);
-    nch = scan_chunks(BF16, bpad_c, tiles, false);
+    nch = scan_chunks(BF16, bpad_c, tiles, false, ku);
     const int tpc = (tiles + nch - 1) / nch;
     if (nch > 256) return false;
     np = (tpc + kListMaxPeriod - 1) / kListMaxPeriod;
@@ -1031,10 +1031,12 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // int16 score image on the re-rank scans (not with the fused re-rank prologue, whose
     // chunk-0 workgroups write the bound while the others already store scores)
     const bool s16_on = s16_env == 1 || (s16_env == 2 && scan4_used(BF16, bpad));
-    int l_nch = 0, l_np = 0, l_G = 0;
-    const bool lgeo = list_geom(bpad, l_nch, l_np, l_G);
-    const bool list_c = lgeo && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
-    const bool list_f = lgeo && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
+    // list geometry per side (the CF side's narrow rows take finer chunks: scan4_list_chunks)
+    int l_nch[2] = {0, 0}, l_np[2] = {0, 0}, l_G[2] = {0, 0};
+    const bool lgeo_c = rr_c && list_geom(bpad, x->Dpad_b * 2 / 16, l_nch[0], l_np[0], l_G[0]);
+    const bool lgeo_f = rr_f && list_geom(bpad, x->Rpad_b * 2 / 16, l_nch[1], l_np[1], l_G[1]);
+    const bool list_c = lgeo_c && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
+    const bool list_f = lgeo_f && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
     // raw-query lists (semantic searches on scan2, f32 query rows, small chunks): the scan
     // rounds the RAW rows to its bf16 operand and the list select normalises them and derives
     // ε itself — no prep launch on the path.  Every item chunk's workgroups convert their
@@ -1049,10 +1051,11 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
                         q->q_dtype == F32 && x->d % 4 == 0 && x->d <= kRrMaxD && rows_c && ((uintptr_t)rows_c & 15) == 0;
     const bool s16_c = !list_c && s16_on && rr_c && !rrfuse_c && gemm_uses_scan(BF16, bpad, x->Dpad_b);
     const bool s16_f = !list_f && s16_on && rr_f && !rrfuse_f && gemm_uses_scan(BF16, bpad, x->Rpad_b);
-    const size_t list_side_b = (size_t)l_nch * l_np * (bpad / 32) * 64 * 16;
+    const size_t list_b[2] = {(size_t)l_nch[0] * l_np[0] * (bpad / 32) * 64 * 16,
+                              (size_t)l_nch[1] * l_np[1] * (bpad / 32) * 64 * 16};
     if ((list_c || list_f) &&
-        ((rc = x->lists.ensure(2 * list_side_b)) ||
-         (list_c && drop && (rc = x->r0lists.ensure((size_t)l_nch * (bpad / 32) * 64 * 8)))))
+        ((rc = x->lists.ensure(list_b[0] + list_b[1])) ||
+         (list_c && drop && (rc = x->r0lists.ensure((size_t)l_nch[0] * (bpad / 32) * 64 * 8)))))
       return rc;
     // the prep launches of both sides (hybrid) go out as one launch
     const bool prep_c = need_content && !fuse_c && !rrfuse_c && !rraw_c, prep_f = need_cf && !fuse_f && !rrfuse_f;
@@ -1130,10 +1133,15 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // select_rr_wave_dual_kernel); each side keeps its own half of the int16 image and its own
     // maxima / flag rows.  Measured (r02za, configs[2]): serial p50 222 -> 173 us (scan 86 ->
     // 77 us, select 116 -> 62 us per step); with three batches in flight 6.6 -> 6.3 M q/s.
-    // BB_DUAL=0 (A/B runs) keeps one launch per side.
-    static const bool dual_env = !(ab_env("BB_DUAL") && atoi(ab_env("BB_DUAL")) == 0);
+    // BB_DUAL=0 (A/B runs) keeps one launch per side.  The list scans (round 4) go out one per
+    // side by default: the CF side's narrow rows now take twice the chunks at two workgroups per
+    // CU (scan4_list_chunks), which one dual launch — held to one workgroup per CU by the
+    // content side's registers — cannot give them (configs[2]: scans 54.1 us dual vs 48.5 us
+    // per side, serial 0.126 vs 0.121 ms, r04p); BB_DUAL=1 forces the dual list scan.
+    static const int dual_sel = ab_env("BB_DUAL") ? atoi(ab_env("BB_DUAL")) : -1;
     static const int sel_wave_env0 = ab_env("BB_SELECT_WAVE") ? atoi(ab_env("BB_SELECT_WAVE")) : -1;
-    const bool dual = dual_env && q->mode == BB_MODE_HYBRID && sides == 2 && ((s16_c && s16_f) || (list_c && list_f)) &&
+    const bool dual = dual_sel != 0 && q->mode == BB_MODE_HYBRID && sides == 2 &&
+                      ((s16_c && s16_f) || (list_c && list_f && dual_sel == 1)) &&
                       !stream &&
                       n_slabs == 1 && scan4_used(BF16, bpad) && scan4_dual_supported((int)x->Dpad_b / 8, (int)x->Rpad_b / 8) &&
                       std::min<int64_t>(slab, x->n) <= 32768 && K_int <= 256 && sel_wave_env0 != 0 && bc > 256;
@@ -1249,10 +1257,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
             ga.q_eps_out = (float*)x->qeps.p;
           }
           if (cf_side ? list_f : list_c) {
-            ga.lists = (uint32_t*)((char*)x->lists.p + (side ? list_side_b : 0));
+            ga.lists = (uint32_t*)((char*)x->lists.p + (cf_side ? list_b[0] : 0));
             ga.r0lists = side_drop ? (uint32_t*)x->r0lists.p : nullptr;
-            ga.l_period = l_G;
-            ga.l_np = l_np;
+            ga.l_period = l_G[cf_side];
+            ga.l_np = l_np[cf_side];
           }
           if (dual && side == 0) {
             ga_dual0 = ga;  // launched with side 1's
@@ -1371,10 +1379,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           sa.s_h = ga.s_h;
           sa.lists = ga.lists;
           sa.r0lists = ga.r0lists;
-          sa.l_chunks = l_nch;
+          sa.l_chunks = l_nch[cf_side];
           sa.l_tiles = ncols_pad / 32;
-          sa.l_np = l_np;
-          sa.l_period = l_G;
+          sa.l_np = l_np[cf_side];
+          sa.l_period = l_G[cf_side];
           sa.l_nb = bpad / 32;
           if (!cf_side && rraw_c) {
             sa.rr_q_raw = rows_c;

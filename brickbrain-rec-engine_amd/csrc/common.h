@@ -402,7 +402,8 @@ bool gemm_uses_scan(int dtype, int Mpad, int Kpad);  // the query-resident scan 
 bool scan3_supported(int Mpad, int Kpad);            // split-bf16 scan for an f32 index
 bool scan4_used(int dtype, int Mpad);                // bf16 scan with 64 queries per wave
 // item chunks (candidate regions / 2 per query) of the scan launch for these shapes
-int scan_chunks(int dtype, int Mpad, int tiles, bool split);
+// item chunks of a scan launch; list_ku > 0: a list scan (kScanList) of rows list_ku 16-B chunks wide
+int scan_chunks(int dtype, int Mpad, int tiles, bool split, int list_ku = 0);
 bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s);  // scan4_used(BF16, a.Mpad) shapes
 int scan4_pilot_m(int kpad);  // GemmArgs.pilot_m of a kScanPilot scan4 launch
 bool scan4_dual_supported(int ku0, int ku1);

@@ -164,7 +164,7 @@ hipError_t launch_gemm(int dtype, const GemmArgs& a, hipStream_t s) {
   // candidate lists: the bf16 scans of a re-rank search (rows up to kRrMaxD wide), periods of
   // at most kListMaxPeriod tiles covering every chunk
   if (a.lists && (!a.s_h || (a.q_istats && !a.q_raw) || a.cand || a.l_period <= 0 || a.l_period > kListMaxPeriod || a.l_np <= 0 ||
-                  (int64_t)a.l_period * a.l_np * scan_chunks(BF16, a.Mpad, a.Ncols / 32, false) < a.Ncols / 32))
+                  (int64_t)a.l_period * a.l_np * scan_chunks(BF16, a.Mpad, a.Ncols / 32, false, a.Kpad * 2 / 16) < a.Ncols / 32))
     return hipErrorInvalidValue;
   // the streaming pilot's top-m maxima: scan4 (bf16), slab mode, no other epilogue output
   if (a.pilot_top && (dtype != BF16 || !scan4_used(BF16, a.Mpad) || !gemm_uses_scan(dtype, a.Mpad, a.Kpad) || a.cand ||

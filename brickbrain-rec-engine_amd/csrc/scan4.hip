@@ -20,14 +20,15 @@ bool scan4_used(int dtype, int Mpad) {
   return dtype == BF16 && Mpad % kScan4Queries == 0 && Mpad >= min_rows && !scan4_env_off();
 }
 
-int scan_chunks(int dtype, int Mpad, int tiles, bool split) {
-  return !split && scan4_used(dtype, Mpad) ? scan4_n_chunks(Mpad, tiles) : scan_n_chunks(Mpad, tiles);
+int scan_chunks(int dtype, int Mpad, int tiles, bool split, int list_ku) {
+  if (split || !scan4_used(dtype, Mpad)) return scan_n_chunks(Mpad, tiles);
+  return list_ku > 0 ? scan4_list_chunks(Mpad, tiles, list_ku) : scan4_n_chunks(Mpad, tiles);
 }
 
 template <int KU>
 static void launch_t(const GemmArgs& a, hipStream_t s) {
   const int tiles = a.Ncols / 32;
-  const int n_chunks = scan4_n_chunks(a.Mpad, tiles);
+  const int n_chunks = a.lists ? scan4_list_chunks(a.Mpad, tiles, KU) : scan4_n_chunks(a.Mpad, tiles);
   const int blocks = a.Mpad / kScan4Queries * n_chunks;
   if constexpr (KU <= kRrMaxD / 8) {
     // the exact re-rank path: the f16 copy of an f32 index
@@ -59,7 +60,8 @@ static void launch_t(const GemmArgs& a, hipStream_t s) {
 template <int KU0, int KU1>
 static void launch_dual_t(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
   const int t0 = a0.Ncols / 32, t1 = a1.Ncols / 32;
-  const int nc0 = scan4_n_chunks(a0.Mpad, t0), nc1 = scan4_n_chunks(a1.Mpad, t1);
+  const int nc0 = a0.lists ? scan4_list_chunks(a0.Mpad, t0, KU0) : scan4_n_chunks(a0.Mpad, t0);
+  const int nc1 = a1.lists ? scan4_list_chunks(a1.Mpad, t1, KU1) : scan4_n_chunks(a1.Mpad, t1);
   const int nb0 = a0.Mpad / kScan4Queries * nc0, nb1 = a1.Mpad / kScan4Queries * nc1;
   if (a0.lists)  // bounded candidate lists on both sides (the f16 re-rank copies)
     bb_launch((scan4_dual_kernel<KU0, KU1, kScanList | kScanF16>), dim3(nb0 + nb1), dim3(kScanWaves * 64), 0,

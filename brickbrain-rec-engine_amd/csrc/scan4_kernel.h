@@ -44,6 +44,18 @@ inline int scan4_n_chunks(int Mpad, int tiles) {
   return n_chunks < tiles ? n_chunks : tiles;
 }
 
+// Item chunks of a list scan (kScanList) of rows KU 16-B chunks wide.  Narrow rows (KU <= 16:
+// the r <= 128 CF factors of a hybrid search) are bound by the list epilogue's VALU, not the
+// MFMA, at one wave per SIMD (configs[2]: the r = 50 scan 22 us beside 33 us for the d = 384
+// content side with six times its MFMA work); their kernel fits two workgroups per CU, so
+// they get twice the chunks (512 workgroups) to fill them.
+inline int scan4_list_chunks(int Mpad, int tiles, int ku) {
+  if (ku > 16) return scan4_n_chunks(Mpad, tiles);
+  const int n_groups = Mpad / kScan4Queries;
+  const int n_chunks = (512 + n_groups - 1) / n_groups;
+  return n_chunks < tiles ? n_chunks : tiles;
+}
+
 // Streaming state of one query (scan2's StreamLane without the region pointer, which is
 // recomputed on the rare append: at d = 768 every VGPR counts).
 struct Stream4 {
