@@ -323,7 +323,7 @@ class ItemIndex:
             rc = fn(h, qp, rp)
             if rc:
                 L.check(rc, "bb_search")
-        run._keep = (keep, q, res)  # keep buffers and structs alive with the closure
+        run._keep = (keep, q, res, self)  # buffers, structs and the index handle live as long as the closure
         return run, out
 
     # ------------------------------------------------------------------ sharded search

@@ -331,3 +331,22 @@ def test_device_inputs_and_views(c1, brickrec):
         assert np.array_equal(out[0].cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
     finally:
         v.close()
+
+
+def test_prepared_search_keeps_its_view_alive(c1):
+    """prepared_search's closure holds the index it searches: dropping the last reference to a
+    view while its prepared search is still in use must not free the handle under it."""
+    import gc
+    import torch
+    idx, x, rows = c1
+    q = torch.from_numpy(R.unit_rows(4, 384, 61)).cuda()
+    v = idx.view()
+    run, out = v.prepared_search("semantic", 10, q_rows=q)
+    del v
+    gc.collect()
+    run()
+    torch.cuda.synchronize()
+    ref = idx.search("semantic", 10, q_rows=q.cpu().numpy())
+    assert np.array_equal(out[1].cpu().numpy(), ref[1])
+    del run
+    gc.collect()
