@@ -153,6 +153,9 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   }
   const int nq4 = a.rr_d >> 2;
   const float hq = a.s_h[row];
+  // (loaded with the lists: the first barrier waits for every outstanding load, so a load
+  // issued after it would stall the bound search's first step instead)
+  const float eps_row = a.rr_eps[row];
   // raw-query lists (GemmArgs.q_raw): wave 0 loads the raw row now and normalises it into
   // the LDS query after the classification (prep_kernel's arithmetic, qnorm.h: the same f32
   // row bit for bit), so its latency hides under the bound search
@@ -202,7 +205,7 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
   __syncthreads();  // hist and misc cleared
   stamp(1);
   // Δ: the re-rank margin in codes (h = 0: a zero query row, every code equal -> take all)
-  const uint32_t delta = hq > 0.f ? (uint32_t)fminf(ceilf(rr_margin(a.rr_eps[row]) / hq), 60000.f) + 2u : 0x10000u;
+  const uint32_t delta = hq > 0.f ? (uint32_t)fminf(ceilf(rr_margin(eps_row) / hq), 60000.f) + 2u : 0x10000u;
 
   // ---- bound: T0 = K-th largest code over every list key, by a bitwise search: each wave
   // counts its lanes' keys >= c with ballots, the four wave counts meet in LDS (two
