@@ -13,9 +13,27 @@ namespace bb {
 
 constexpr int kQnC = 8;  // elements per lane: rows up to 64·8 = 512 wide
 
+// f64 lane value from `CTRL`'s DPP source lane (both halves moved; every lane active)
+template <int CTRL>
+__device__ __forceinline__ double qn_dpp(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// Wave sum by the xor butterfly 32, 16, 8, 4, 2, 1.  The last four steps are DPP row rotations
+// (row_ror 8, 4, 2, 1): after the steps above them a lane's value equals its partners' at the
+// xor distances already summed, so the rotation reads the same value the xor partner holds —
+// the same additions in the same order as __shfl_xor at every step (the same bits), without
+// the LDS permute round trips.  Every lane of the wave must be active.
 __device__ __forceinline__ double qn_wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  v += __shfl_xor(v, 32);
+  v += __shfl_xor(v, 16);
+  v += qn_dpp<0x128>(v);  // row_ror:8
+  v += qn_dpp<0x124>(v);  // row_ror:4
+  v += qn_dpp<0x122>(v);  // row_ror:2
+  v += qn_dpp<0x121>(v);  // row_ror:1
   return v;
 }
 
