@@ -825,6 +825,207 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
   else wave_sort_emit<8>(sel, m, sa, row, drop);
 }
 
+// ---- streaming top-K, second stage: one wave per query ---------------------------------------
+// The workgroup-per-query kernel above spends its time in a full bitonic sort of every
+// candidate (~8·K_int per query at configs[3]) by four waves and a merge by binary searches.
+// Here one wave owns a query and only finds the K-th largest key: the candidates sit in
+// registers (up to 2,048 per wave, 32 per lane), the K-th largest score image by bisection
+// over its 32 bits (per step: a compare and a ballot popcount per register — no LDS, no
+// barriers), starting below the common prefix of the smallest and largest image; equal
+// images at the K-th place (rare) are split by a second bisection over the item word.  The
+// K keys above it are compacted by ballot and sorted by wave_sort_emit.  More than 2,048
+// candidates (a bound far from the data): the top K of every 2,048-key page, then the top K
+// of those; past kMaxKInt survivors, the bisection over pages re-read at every step.  Same
+// outputs as cand_select_kernel, bit for bit.
+constexpr int kCswWaves = kSelectThreads / 64;  // queries per workgroup
+constexpr int kCswNJ = 32;                      // candidate registers per lane (2,048 per wave)
+
+template <int NJ, typename Fetch>
+__device__ __forceinline__ int csw_select(Fetch fetch, int n, uint32_t K, uint64_t* sel, int lane) {
+  const int pages = (n + 64 * NJ - 1) / (64 * NJ);
+  uint64_t v[NJ];
+  auto load = [&](int pg) __attribute__((always_inline)) {
+    int idx[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) idx[j] = pg * 64 * NJ + j * 64 + lane;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) v[j] = idx[j] < n ? fetch(idx[j]) : 0ull;
+  };
+  // keys satisfying pred over all pages (real keys have a non-zero score image; empty slots 0)
+  auto count = [&](auto pred) __attribute__((always_inline)) {
+    uint32_t c = 0;
+    for (int pg = 0; pg < pages; ++pg) {
+      if (pages > 1) load(pg);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) c += (uint32_t)__popcll(__ballot(pred(v[j])));
+    }
+    return c;
+  };
+  load(0);
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  for (int pg = 0; pg < pages; ++pg) {
+    if (pages > 1) load(pg);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const uint32_t h = (uint32_t)(v[j] >> 32);
+      mn = v[j] && h < mn ? h : mn;
+      mx = h > mx ? h : mx;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t a = (uint32_t)__shfl_xor((int)mn, o), b = (uint32_t)__shfl_xor((int)mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  // p = the K-th largest image: the largest t with count(image >= t) >= K; mn <= p <= mx, so
+  // the bits above their highest differing bit are fixed
+  const uint32_t d = mn ^ mx;
+  const int hb = d ? 31 - __builtin_clz(d) : -1;
+  uint32_t p = hb < 0 ? mx : hb >= 31 ? 0u : (mx & ~((2u << hb) - 1u));
+  for (int b = hb; b >= 0; --b) {
+    const uint32_t t = p | (1u << b);
+    if (count([&](uint64_t k) { return (uint32_t)(k >> 32) >= t; }) >= K) p = t;
+  }
+  const uint32_t c_ge = count([&](uint64_t k) { return (uint32_t)(k >> 32) >= p; });
+  uint32_t pl = 0u;  // item word bound among the keys whose image is p (when they tie there)
+  if (c_ge > K) {
+    const uint32_t need = K - count([&](uint64_t k) { return (uint32_t)(k >> 32) > p; });
+    for (int b = 31; b >= 0; --b) {
+      const uint32_t t = pl | (1u << b);
+      if (count([&](uint64_t k) { return (uint32_t)(k >> 32) == p && (uint32_t)k >= t; }) >= need) pl = t;
+    }
+  }
+  const uint64_t kth = ((uint64_t)p << 32) | pl;
+  uint32_t m = 0;
+  for (int pg = 0; pg < pages; ++pg) {
+    if (pages > 1) load(pg);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const bool take = v[j] >= kth;
+      const uint64_t bal = __ballot(take);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      if (take && m + below < (uint32_t)kMaxKInt) sel[m + below] = v[j];
+      m += (uint32_t)__popcll(bal);
+    }
+  }
+  return (int)(m < (uint32_t)kMaxKInt ? m : (uint32_t)kMaxKInt);
+}
+
+__global__ __launch_bounds__(kSelectThreads) void cand_select_wave_kernel(CandSelectArgs a, int B) {
+  __shared__ uint32_t pre_all[kCswWaves][kCsRegionsMax + 1];
+  __shared__ __attribute__((aligned(16))) uint64_t sel_all[kCswWaves][kMaxKInt];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = xcd_row(blockIdx.x, gridDim.x) * kCswWaves + wave;
+  if (row >= B) return;  // whole wave; no workgroup barriers below
+  uint32_t* pre = pre_all[wave];
+  uint64_t* sel = sel_all[wave];
+  const int R = a.regions, Q = (R + 63) >> 6;  // regions per lane, consecutive
+  const size_t rbase = (size_t)row * R;
+  uint32_t c[16], sum = 0, ovf = 0;
+  uint64_t gm = (a.cand_pmax && a.max_in && lane == 0) ? a.max_in[row] : 0ull;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int r = lane * Q + q;
+    const bool in = q < Q && r < R;
+    const uint32_t raw = in ? a.cand_cnt[rbase + r] : 0u;
+    ovf |= raw > (uint32_t)a.cap ? 1u : 0u;
+    c[q] = raw < (uint32_t)a.cap ? raw : (uint32_t)a.cap;
+    sum += c[q];
+    if (a.cand_pmax && in) {
+      const uint64_t k = a.cand_pmax[rbase + r];
+      gm = k > gm ? k : gm;
+    }
+  }
+  if (__any(ovf) && lane == 0) atomicOr(a.overflow, 1u);
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+    incl += lane >= o ? y : 0u;
+  }
+  const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+  uint32_t off = incl - sum;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int r = lane * Q + q;
+    if (q < Q && r < R) pre[r] = off;
+    off += c[q];
+  }
+  if (lane == 0) pre[R] = total;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t y = __shfl_xor(gm, o);
+    gm = y > gm ? y : gm;
+  }
+  const uint64_t gmax = a.cand_pmax ? gm : 0ull;
+  if (a.cand_pmax && a.max_out && lane == 0) a.max_out[row] = gmax;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  const uint64_t* carry = a.carry_in ? a.carry_in + (size_t)row * a.K : nullptr;
+  int top = 1;  // the largest power of two <= R
+  while (2 * top <= R) top <<= 1;
+  // candidate i -> its region (the last region starting at or below i) and slot
+  auto fetch = [&](int i) __attribute__((always_inline)) -> uint64_t {
+    if (i >= (int)total) return carry[i - (int)total];
+    int lo = 0;
+    for (int st = top; st > 0; st >>= 1) {
+      const int m = lo + st;
+      if (m < R && pre[m] <= (uint32_t)i) lo = m;
+    }
+    return a.cand[(rbase + lo) * (size_t)a.cap + (i - (int)pre[lo])];
+  };
+  const int n = (int)total + (carry ? a.K : 0);
+  int m;
+  if (n <= a.K || n <= 256) {  // every candidate goes to the sort (n <= kMaxKInt)
+    for (int i = lane; i < n; i += 64) sel[i] = fetch(i);
+    m = n;
+  } else if (n <= 512) {
+    m = csw_select<8>(fetch, n, (uint32_t)a.K, sel, lane);
+  } else if (n <= 1024) {
+    m = csw_select<16>(fetch, n, (uint32_t)a.K, sel, lane);
+  } else if (n <= 64 * kCswNJ) {
+    m = csw_select<kCswNJ>(fetch, n, (uint32_t)a.K, sel, lane);
+  } else if ((n + 64 * kCswNJ - 1) / (64 * kCswNJ) * a.K <= kMaxKInt) {
+    // more than 2,048: the top K of each 2,048-key page (the global top K is among them),
+    // then the top K of those survivors — every step on registers, no re-reads
+    int ms = 0;
+    for (int b0 = 0; b0 < n; b0 += 64 * kCswNJ) {
+      const int np = min(64 * kCswNJ, n - b0);
+      auto fp = [&](int i) __attribute__((always_inline)) { return fetch(b0 + i); };
+      if (np <= a.K) {
+        for (int i = lane; i < np; i += 64) sel[ms + i] = fp(i);
+        ms += np;
+      } else {
+        ms += csw_select<kCswNJ>(fp, np, (uint32_t)a.K, sel + ms, lane);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    auto fs = [&](int i) __attribute__((always_inline)) { return sel[i]; };
+    m = ms <= a.K ? ms : csw_select<8>(fs, ms, (uint32_t)a.K, sel, lane);  // ms <= kMaxKInt
+  } else {  // (pages·K > kMaxKInt) the bisection over pages re-read at every step
+    m = csw_select<kCswNJ>(fetch, n, (uint32_t)a.K, sel, lane);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  SelectArgs sa{};
+  sa.K = a.K;
+  sa.keys_out = a.keys_out;
+  sa.out_scores = a.out_scores;
+  sa.out_ids = a.out_ids;
+  sa.out_counts = a.out_counts;
+  sa.k_final = a.k_final;
+  if (m <= 64) wave_sort_emit<1>(sel, m, sa, row, gmax);
+  else if (m <= 128) wave_sort_emit<2>(sel, m, sa, row, gmax);
+  else if (m <= 256) wave_sort_emit<4>(sel, m, sa, row, gmax);
+  else wave_sort_emit<8>(sel, m, sa, row, gmax);
+}
+
 // ---- exact re-rank, second stage (SelectArgs.rr_*) ------------------------------------------
 // One workgroup per query: the exact rank 0 from its approximate candidates, then the
 // candidates within 2ε of the K-th approximate score rescored from the f32 rows (16-lane
@@ -1234,7 +1435,11 @@ hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s) {
   if (a.K <= 0 || a.K > kMaxKInt || B <= 0 || a.regions <= 0 || a.regions > kCsRegionsMax || a.cap <= 0 ||
       !a.cand || !a.cand_cnt || !a.overflow || (!a.out_scores && !a.keys_out))
     return hipErrorInvalidValue;
-  bb_launch(cand_select_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
+  static const bool wg_path = ab_env("BB_CS_WG") != nullptr;  // A/B: the workgroup-per-query kernel
+  if (wg_path)
+    bb_launch(cand_select_kernel, dim3(B), dim3(kSelectThreads), 0, s, a);
+  else
+    bb_launch(cand_select_wave_kernel, dim3((B + kCswWaves - 1) / kCswWaves), dim3(kSelectThreads), 0, s, a, B);
   return hipGetLastError();
 }
 

@@ -273,3 +273,52 @@ def test_stream_two_level_bound(brickrec, dtype, mode):
     if mode == "similar":
         for i in range(B):
             assert qi[i] not in set(a[1][i]) and mask[a[1][i]].all()
+
+
+def test_stream_ties_at_kth(brickrec):
+    """Every row present 24 times (bf16, 384-d; the copies spread over the index, so no
+    candidate region collects them all): equal scores straddle the K-th place of almost
+    every query, so the candidate select's second bisection (item word among equal score
+    images) decides the list; stream == slab exactly (ids ascending among equals)."""
+    base = R.unit_rows(5000, 384, 71)
+    x = np.tile(base, (24, 1))                 # 120,000 rows
+    q = R.unit_rows(160, 384, 72)
+    idx = brickrec.ItemIndex(dtype="bf16")
+    idx.upload_items(x)
+    (sc, ids, cnt), slab = _both(idx, "semantic", 50, stream_gemms=2, q_rows=q)
+    _same((sc, ids, cnt), slab)
+    assert np.all(cnt == 50)
+    ties = sum(int(np.sum(sc[i] == sc[i][-1])) > 1 for i in range(len(q)))
+    assert ties > len(q) // 2, ties   # the tie path ran for most rows
+
+
+def test_stream_many_candidates_paged(brickrec):
+    """top-300 (K_int 301): ~8·K_int = 2,400 candidates per query, more than the 2,048 a
+    wave of the candidate select holds in registers — the paged bisection; stream == slab
+    exactly on a bf16 index (the slab path selects from the score image, not from candidates)."""
+    n, d, B, k = 125000, 768, 96, 300
+    x = R.unit_rows(n, d, 73)
+    q = R.unit_rows(B, d, 74)
+    idx = brickrec.ItemIndex(dtype="bf16")
+    idx.upload_items(x)
+    (sc, ids, cnt), slab = _both(idx, "semantic", k, stream_gemms=2, q_rows=q)
+    _same((sc, ids, cnt), slab)
+    assert np.all(cnt == k)
+    for i in range(0, B, 16):
+        assert np.all(np.diff(sc[i]) <= 0)
+        assert set(ids[i]) == set(np.unique(ids[i]))
+
+
+def test_stream_small_pilot_pages(brickrec):
+    """A 2 MiB workspace holds a pilot of a few thousand rows of 125,000: ~30·K_int = 3,000
+    candidates per query for top-100 — two 2,048-key pages of the candidate select, each
+    reduced to its top K_int before the final bisection; stream == slab exactly (bf16)."""
+    n, d, B, k = 125000, 768, 96, 100
+    x = R.unit_rows(n, d, 75)
+    q = R.unit_rows(B, d, 76)
+    idx = brickrec.ItemIndex(dtype="bf16")
+    idx.upload_items(x)
+    idx.set_option("workspace_bytes", 2 << 20)
+    (sc, ids, cnt), slab = _both(idx, "semantic", k, stream_gemms=2, q_rows=q)
+    _same((sc, ids, cnt), slab)
+    assert np.all(cnt == k)
