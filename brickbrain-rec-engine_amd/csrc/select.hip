@@ -834,7 +834,7 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
 // barriers), starting below the common prefix of the smallest and largest image; equal
 // images at the K-th place (rare) are split by a second bisection over the item word.  The
 // K keys above it are compacted by ballot and sorted by wave_sort_emit.  More than 2,048
-// candidates (a bound far from the data): the top K of every 2,048-key page, then the top K
+// candidates (a bound far from the data): the top K of every 1,024-key page, then the top K
 // of those; past kMaxKInt survivors, the bisection over pages re-read at every step.  Same
 // outputs as cand_select_kernel, bit for bit.
 constexpr int kCswWaves = kSelectThreads / 64;  // queries per workgroup
@@ -988,18 +988,19 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_wave_kernel(CandSe
     m = csw_select<16>(fetch, n, (uint32_t)a.K, sel, lane);
   } else if (n <= 64 * kCswNJ) {
     m = csw_select<kCswNJ>(fetch, n, (uint32_t)a.K, sel, lane);
-  } else if ((n + 64 * kCswNJ - 1) / (64 * kCswNJ) * a.K <= kMaxKInt) {
-    // more than 2,048: the top K of each 2,048-key page (the global top K is among them),
-    // then the top K of those survivors — every step on registers, no re-reads
+  } else if ((n + 1023) / 1024 * a.K <= kMaxKInt) {
+    // more than 2,048: the top K of each 1,024-key page (the global top K is among them),
+    // then the top K of those survivors — every step on registers, no re-reads (pages of
+    // 1,024, not 2,048: a second 32-register set would cost the kernel a wave per SIMD)
     int ms = 0;
-    for (int b0 = 0; b0 < n; b0 += 64 * kCswNJ) {
-      const int np = min(64 * kCswNJ, n - b0);
+    for (int b0 = 0; b0 < n; b0 += 1024) {
+      const int np = min(1024, n - b0);
       auto fp = [&](int i) __attribute__((always_inline)) { return fetch(b0 + i); };
       if (np <= a.K) {
         for (int i = lane; i < np; i += 64) sel[ms + i] = fp(i);
         ms += np;
       } else {
-        ms += csw_select<kCswNJ>(fp, np, (uint32_t)a.K, sel + ms, lane);
+        ms += csw_select<16>(fp, np, (uint32_t)a.K, sel + ms, lane);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
