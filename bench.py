@@ -411,11 +411,16 @@ def make_lane(brickrec, workload, base, B, local, dev, rank, j, inflight, extra)
         u = rng.normal(0.0, 0.1, (B, extra["f"].shape[1])).astype(np.float32)
         mw = torch.from_numpy(brickrec.bits_from_bool(mask).view(np.int32)).to(dev)
         ew = torch.from_numpy(brickrec.bits_from_bool(rated).view(np.int32)).to(dev)
-        run, outs = idx.prepared_search("hybrid", TOPK, q_items=torch.from_numpy(liked).to(dev),
-                                        q_cf=torch.from_numpy(u).to(dev), mask=mw, excl=ew, stream=s)
+        kw = dict(q_items=torch.from_numpy(liked).to(dev), q_cf=torch.from_numpy(u).to(dev), mask=mw, excl=ew,
+                  stream=s)
+        run, outs = idx.prepared_search("hybrid", TOPK, **kw)
+        # the profiled runs go through bb_search on the lane's own handle (a plan replays on its
+        # private view, which the lane's profiler does not see): the same kernels and arguments
+        run.prof_run = idx.prepared_search("hybrid", TOPK, plan=False, **kw)[0]
         return idx, s, run, outs, {"liked": liked, "rated": rated, "u": u, "mask": np.asarray(mask, bool)}
     q = unit_rows_torch(B, DIM, 4321 + rank + 1000 * j, dev)
     run, outs = idx.prepared_search("semantic", TOPK, q_rows=q, stream=s)
+    run.prof_run = idx.prepared_search("semantic", TOPK, q_rows=q, stream=s, plan=False)[0]
     return idx, s, run, outs, q
 
 
@@ -659,7 +664,7 @@ def main():
     # at a time (lane 0 alone: kernel averages not inflated by the other lanes' batches) ----
     idx.set_profiling(True)
     for _ in range(args.steps):
-        run()
+        run.prof_run()
     prof = idx.profile()
     idx.set_profiling(False)
     fam_us = {k: 1e3 * v["ms"] / max(args.steps, 1) for k, v in prof.items() if v["launches"]}

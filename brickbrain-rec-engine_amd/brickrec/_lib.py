@@ -25,7 +25,8 @@ BB_OK, BB_E_ARG, BB_E_HIP, BB_E_STATE, BB_E_NOMEM = 0, -1, -2, -3, -4
 # every entry point include/brickrec.h declares (checked by tests/test_abi.py)
 EXPORTS = ("bb_create", "bb_upload_items", "bb_upload_cf", "bb_upload_attrs", "bb_eval_mask",
            "bb_search", "bb_key_lens", "bb_finalize", "bb_set_profiling", "bb_get_profile", "bb_set_option",
-           "bb_info", "bb_get_rows", "bb_create_view", "bb_destroy", "bb_last_error", "bb_abi_version")
+           "bb_info", "bb_get_rows", "bb_create_view", "bb_destroy", "bb_last_error", "bb_abi_version",
+           "bb_plan_create", "bb_plan_launch", "bb_plan_destroy")
 
 
 class BrickrecError(RuntimeError):
@@ -98,6 +99,9 @@ def load() -> C.CDLL:
             "bb_get_rows": ([P, P, C.c_int32, P, C.c_int32], C.c_int),
             "bb_create_view": ([P, C.POINTER(P)], C.c_int),
             "bb_destroy": ([P], C.c_int),
+            "bb_plan_create": ([P, C.POINTER(bb_query), C.POINTER(bb_result), C.POINTER(P)], C.c_int),
+            "bb_plan_launch": ([P], C.c_int),
+            "bb_plan_destroy": ([P], C.c_int),
             "bb_last_error": ([], C.c_char_p),
             "bb_abi_version": ([], C.c_int),
         }

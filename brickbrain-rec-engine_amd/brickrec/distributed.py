@@ -177,8 +177,9 @@ class ShardedIndex:
             return None
         ndim = 2 if rows else 1
         is_t = isinstance(a, torch.Tensor)
-        dt = a.dtype
-        if (is_t and dt == torch.bool) or (not is_t and np.asarray(a).dtype == np.bool_):
+        if not is_t:
+            a = np.asarray(a)   # lists / tuples of bools or packed words
+        if (is_t and a.dtype == torch.bool) or (not is_t and a.dtype == np.bool_):
             from .engine import bits_from_bool
             g = np.asarray(a.cpu() if is_t else a, bool)
             if g.ndim != ndim or g.shape[-1] not in (self.n, self.n_local):

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 import threading
+import weakref
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
@@ -73,6 +74,41 @@ class Predicate:
     excluded_items: Sequence[int] = ()  # global ids
 
 
+class _Plan:
+    """A prepared search (bb_plan_create): calling it replays the recorded launches
+    (bb_plan_launch).  It holds its inputs, outputs and index alive; close() (or garbage
+    collection, or closing the index) destroys the plan and its private view."""
+
+    def __init__(self, lib, handle, root, keep):
+        self._lib, self._p, self._root, self._keep = lib, handle, root, keep
+        self._launch = lib.bb_plan_launch
+        if not hasattr(root, "_plans"):
+            root._plans = weakref.WeakSet()
+        root._plans.add(self)
+
+    def __call__(self):
+        rc = self._launch(self._p)
+        if rc:
+            L.check(rc, "bb_plan_launch")
+
+    def close(self):
+        p, self._p = getattr(self, "_p", None), None
+        if not p:
+            return
+        root = self._root
+        rc = self._lib.bb_plan_destroy(p)
+        with root._mu:
+            root._views -= 1
+        getattr(root, "_plans", set()).discard(self)
+        L.check(rc, "bb_plan_destroy")
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ItemIndex:
     def __init__(self, device: int = 0, dtype: str = "f32", id_offset: int = 0,
                  workspace_bytes: int = 0):
@@ -113,6 +149,8 @@ class ItemIndex:
         mu = getattr(self, "_mu", None)
         if mu is None:
             return
+        for p in list(getattr(self, "_plans", ())):
+            p.close()
         with mu:
             if not getattr(self, "_h", None):
                 return
@@ -296,9 +334,12 @@ class ItemIndex:
 
     def prepared_search(self, mode: str, k: int, *, q_rows=None, q_items=None, q_cf=None,
                         mask=None, excl=None, k_side: int = 0, w_content=0.4, w_cf=0.6,
-                        stream=None):
-        """Build the ctypes structures once for repeated device-resident calls (bench loop).
-        All inputs must be torch CUDA tensors of the right dtypes; returns (run, outputs)."""
+                        stream=None, plan: bool = True):
+        """A repeated device-resident search (the serving loop; bench).  All inputs must be
+        torch CUDA tensors of the right dtypes; returns (run, outputs): each run() searches
+        the inputs' current contents into the same outputs.  With plan=True (default) run is a
+        bb_plan (include/brickrec.h): the host logic ran once, run() replays the launches; with
+        plan=False (or a search the plan refuses) run() calls bb_search."""
         import torch
         first = next(x for x in (q_rows, q_items, q_cf) if x is not None)
         dev, B = first.device, int(first.shape[0])
@@ -317,6 +358,21 @@ class ItemIndex:
                         excl.data_ptr() if excl is not None else None, w_content, w_cf,
                         s.cuda_stream, _null(s))
         res = L.bb_result(out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), L.BB_DEVICE, None, None)
+        if plan:
+            # bb_plan_create: the host side of the search runs once; each call replays its
+            # launches.  Searches that synchronise with the host (the streaming top-K) refuse a
+            # plan (BB_E_STATE) and keep the bb_search call below.
+            root = getattr(self, "_base", None) or self
+            ph = C.c_void_p()
+            with root._mu, self._mu:
+                rc = self._lib.bb_plan_create(self._h, C.byref(q), C.byref(res), C.byref(ph))
+                if rc == 0:
+                    root._views = getattr(root, "_views", 0) + 1   # the plan's private view
+            if rc == 0:
+                p = _Plan(self._lib, ph, root, (keep, q, res, self))
+                return p, out
+            if rc != L.BB_E_STATE:
+                L.check(rc, "bb_plan_create")
         fn, h, qp, rp = self._lib.bb_search, self._h, C.byref(q), C.byref(res)
 
         def run():

@@ -12,6 +12,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/brickrec.h"
@@ -54,6 +55,8 @@ struct DevBuf {
   int ensure(size_t bytes) {
     if (bytes <= cap) return BB_OK;
     if (!owned) return fail(BB_E_STATE, "a view cannot resize its base's buffers");
+    // a plan being recorded keeps every pointer it captured: no buffer may move under it
+    if (p && tl_capture) return fail(BB_E_STATE, "bb_plan_create: a workspace buffer regrew within the search");
     if (p) {
       hipError_t e = hipFree(p);
       if (e != hipSuccess) return fail(BB_E_HIP, std::string("hipFree: ") + hipGetErrorString(e));
@@ -76,9 +79,33 @@ struct DevBuf {
   }
 };
 
+// Live handles (bb_create / bb_create_view / bb_plan_create add, bb_destroy / bb_plan_destroy
+// remove): every entry point checks its handle here before touching it, so a destroyed, foreign
+// or corrupted pointer returns BB_E_ARG instead of crashing the caller's process (ADVICE / VERDICT
+// r04: a use-after-free reached bb_search from a dropped Python view).  The magic word is
+// checked only after the set says the pointer is ours (a freed pointer is never dereferenced).
+constexpr uint64_t kIndexMagic = 0x3130786469626262ull;  // "bbbidx01"
+constexpr uint64_t kPlanMagic = 0x31306e616c706262ull;   // "bbplan01"
+std::mutex g_live_mu;
+std::unordered_set<const void*> g_live;
+
+void live_add(const void* p) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  g_live.insert(p);
+}
+bool live_del(const void* p) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  return g_live.erase(p) != 0;
+}
+bool live_has(const void* p) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  return g_live.count(p) != 0;
+}
+
 }  // namespace
 
 struct bb_index {
+  uint64_t magic = kIndexMagic;
   int device = 0;
   int dtype = F32;
   int64_t id_offset = 0;
@@ -138,7 +165,76 @@ struct bb_index {
   int64_t launches[K_NFAM] = {0};
 };
 
+// A prepared search (bb_plan_create): the launches of one recorded search, replayed as they
+// are.  It owns a private view of the index (own stream, own workspace) so no other call can
+// move or overwrite the buffers its launches were recorded with.
+struct bb_plan {
+  uint64_t magic = kPlanMagic;
+  bb_index* view = nullptr;
+  int device = 0;
+  hipStream_t s = nullptr;
+  std::vector<bb::CapturedOp> ops;
+  std::vector<std::vector<void*>> argv;  // per launch: pointers into its argument blob
+};
+
 namespace {
+
+// Handle checks of the entry points (see g_live above).
+int check_index(const bb_index* x, const char* fn) {
+  if (!x) return fail(BB_E_ARG, std::string(fn) + ": null index");
+  if (!live_has(x) || x->magic != kIndexMagic)
+    return fail(BB_E_ARG, std::string(fn) + ": stale or foreign index handle (destroyed, or not from bb_create)");
+  return BB_OK;
+}
+int check_plan(const bb_plan* p, const char* fn) {
+  if (!p) return fail(BB_E_ARG, std::string(fn) + ": null plan");
+  if (!live_has(p) || p->magic != kPlanMagic)
+    return fail(BB_E_ARG, std::string(fn) + ": stale or foreign plan handle (destroyed, or not from bb_plan_create)");
+  return BB_OK;
+}
+#define BB_CHECK_INDEX(x, fn)                \
+  do {                                       \
+    const int rc__ = check_index((x), (fn)); \
+    if (rc__) return rc__;                   \
+  } while (0)
+
+// Stream operations of a search: while a plan is recorded (tl_capture) the copies and fills
+// join the record and a host synchronisation fails the plan (the streaming top-K reads its
+// overflow flag on the host; host buffers are synchronised) — such searches stay bb_search's.
+int s_memset(void* p, int v, size_t bytes, hipStream_t s) {
+  if (tl_capture) {
+    CapturedOp op;
+    op.kind = 1;
+    op.dst = p;
+    op.value = v;
+    op.bytes = bytes;
+    tl_capture->push_back(std::move(op));
+    return BB_OK;
+  }
+  BB_HIP(hipMemsetAsync(p, v, bytes, s));
+  return BB_OK;
+}
+int s_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+  if (tl_capture) {
+    if (kind != hipMemcpyDeviceToDevice) return fail(BB_E_STATE, "bb_plan_create: the search copies to the host");
+    CapturedOp op;
+    op.kind = 2;
+    op.dst = dst;
+    op.src = src;
+    op.bytes = bytes;
+    tl_capture->push_back(std::move(op));
+    return BB_OK;
+  }
+  BB_HIP(hipMemcpyAsync(dst, src, bytes, kind, s));
+  return BB_OK;
+}
+int s_sync(hipStream_t s) {
+  if (tl_capture)
+    return fail(BB_E_STATE, "bb_plan_create: this search synchronises with the host (the streaming top-K of a large "
+                            "index): use bb_search");
+  BB_HIP(hipStreamSynchronize(s));
+  return BB_OK;
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -293,12 +389,14 @@ int bb_create(const bb_desc* desc, bb_index** out) {
     delete x;
     return fail(BB_E_HIP, std::string("hipEventCreate: ") + hipGetErrorString(e));
   }
+  live_add(x);
   *out = x;
   return BB_OK;
 }
 
 int bb_create_view(bb_index* b, bb_index** out) {
-  if (!b || !out) return fail(BB_E_ARG, "bb_create_view: null argument");
+  BB_CHECK_INDEX(b, "bb_create_view");
+  if (!out) return fail(BB_E_ARG, "bb_create_view: null argument");
   *out = nullptr;
   if (b->base) return fail(BB_E_ARG, "bb_create_view: the base is itself a view");
   std::lock_guard<std::mutex> lk(b->mu);
@@ -340,10 +438,12 @@ int bb_create_view(bb_index* b, bb_index** out) {
 
 int bb_destroy(bb_index* x) {
   if (!x) return BB_OK;
+  BB_CHECK_INDEX(x, "bb_destroy");
   {
     std::lock_guard<std::mutex> lk(x->mu);  // bb_create_view counts views under it
-    if (x->n_views > 0) return fail(BB_E_STATE, "bb_destroy: destroy the index's views first");
+    if (x->n_views > 0) return fail(BB_E_STATE, "bb_destroy: destroy the index's views (and plans) first");
   }
+  live_del(x);
   {
     DeviceGuard g(x->device);
     // a view's kernels read its base's rows: they finish before the base may be destroyed
@@ -372,12 +472,13 @@ int bb_destroy(bb_index* x) {
     (void)hipEventDestroy(x->done);
     (void)hipStreamDestroy(x->stream);
   }
+  x->magic = 0;  // poisoned (the allocator may hand the memory out again)
   delete x;
   return BB_OK;
 }
 
 int bb_info(bb_index* x, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* r) {
-  if (!x) return fail(BB_E_ARG, "null index");
+  BB_CHECK_INDEX(x, "bb_info");
   if (n_items) *n_items = x->n;
   if (d) *d = x->d;
   if (d_pad) *d_pad = x->Dpad;
@@ -386,7 +487,8 @@ int bb_info(bb_index* x, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* 
 }
 
 int bb_get_rows(bb_index* x, const int64_t* ids, int32_t B, void* out, int32_t where) {
-  if (!x || !ids || !out || B <= 0) return fail(BB_E_ARG, "bb_get_rows: bad arguments");
+  BB_CHECK_INDEX(x, "bb_get_rows");
+  if (!ids || !out || B <= 0) return fail(BB_E_ARG, "bb_get_rows: bad arguments");
   if (x->n <= 0) return fail(BB_E_STATE, "no items uploaded");
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
@@ -484,8 +586,9 @@ static int make_rr(bb_index* x, DevBuf& rows, DevBuf& bf, int ld, int& ld_b, int
 
 int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t in_dtype, int32_t prenormalized,
                     int32_t where, const uint32_t* present_bits) {
-  if (x && x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
-  if (!x || !rows || n <= 0 || d <= 0) return fail(BB_E_ARG, "bb_upload_items: bad arguments");
+  BB_CHECK_INDEX(x, "bb_upload_items");
+  if (x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
+  if (!rows || n <= 0 || d <= 0) return fail(BB_E_ARG, "bb_upload_items: bad arguments");
   if (in_dtype != F32 && in_dtype != BF16 && in_dtype != F64) return fail(BB_E_ARG, "bad input dtype");
   if (n >= 0xFFFFFFFFll - x->id_offset) return fail(BB_E_ARG, "too many items for 32-bit ids");
   std::lock_guard<std::mutex> lk(x->mu);  // bb_create_view takes it too
@@ -520,8 +623,9 @@ int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t
 }
 
 int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const uint32_t* present_bits) {
-  if (x && x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
-  if (!x || !f || r <= 0) return fail(BB_E_ARG, "bb_upload_cf: bad arguments");
+  BB_CHECK_INDEX(x, "bb_upload_cf");
+  if (x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
+  if (!f || r <= 0) return fail(BB_E_ARG, "bb_upload_cf: bad arguments");
   if (x->n <= 0) return fail(BB_E_STATE, "upload items before CF factors");
   std::lock_guard<std::mutex> lk(x->mu);  // bb_create_view takes it too
   if (x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
@@ -550,8 +654,9 @@ int bb_upload_cf(bb_index* x, const void* f, int32_t r, int32_t in_dtype, const 
 }
 
 int bb_upload_attrs(bb_index* x, const int32_t* num_parts, const int16_t* year, const int32_t* theme_id) {
-  if (x && x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
-  if (!x || !num_parts || !year || !theme_id) return fail(BB_E_ARG, "bb_upload_attrs: bad arguments");
+  BB_CHECK_INDEX(x, "bb_upload_attrs");
+  if (x->base) return fail(BB_E_STATE, "a view shares its base's rows: upload to the base");
+  if (!num_parts || !year || !theme_id) return fail(BB_E_ARG, "bb_upload_attrs: bad arguments");
   if (x->n <= 0) return fail(BB_E_STATE, "upload items before attributes");
   std::lock_guard<std::mutex> lk(x->mu);  // bb_create_view takes it too
   if (x->n_views > 0) return fail(BB_E_STATE, "the index has live views: destroy them before uploading");
@@ -569,7 +674,8 @@ int bb_upload_attrs(bb_index* x, const int32_t* num_parts, const int16_t* year, 
 }
 
 int bb_eval_mask(bb_index* x, const bb_predicate* p, uint32_t* out_bits, int32_t where) {
-  if (!x || !p || !out_bits) return fail(BB_E_ARG, "bb_eval_mask: bad arguments");
+  BB_CHECK_INDEX(x, "bb_eval_mask");
+  if (!p || !out_bits) return fail(BB_E_ARG, "bb_eval_mask: bad arguments");
   if (!x->parts.p) return fail(BB_E_STATE, "upload attributes before evaluating masks");
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
@@ -860,9 +966,12 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     }
     if (out_keys) {
       const hipMemcpyKind kind = res->where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-      BB_HIP(hipMemcpyAsync(res->keys, x->keys.p, (size_t)sides * B * K_int * 8, kind, s));
-      if (drop) BB_HIP(hipMemcpyAsync(res->max_keys, x->maxk.p, (size_t)B * 8, kind, s));
-      else if (res->where == BB_DEVICE) BB_HIP(hipMemsetAsync(res->max_keys, 0, (size_t)B * 8, s));
+      if ((rc = s_copy(res->keys, x->keys.p, (size_t)sides * B * K_int * 8, kind, s))) return rc;
+      if (drop) {
+        if ((rc = s_copy(res->max_keys, x->maxk.p, (size_t)B * 8, kind, s))) return rc;
+      } else if (res->where == BB_DEVICE) {
+        if ((rc = s_memset(res->max_keys, 0, (size_t)B * 8, s))) return rc;
+      }
       else memset(res->max_keys, 0, (size_t)B * 8);
     } else if (hyb) {  // the union blend of _combine_recommendations (:789-843), as the large-batch path
       FinalizeArgs fa{};
@@ -889,7 +998,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       BB_HIP(hipMemcpyAsync(res->ids, f_id, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
       if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, f_cnt, (size_t)B * 4, hipMemcpyDeviceToHost, s));
     }
-    if (host_res || where == BB_HOST || (out_keys && res->where != BB_DEVICE)) BB_HIP(hipStreamSynchronize(s));
+    if (host_res || where == BB_HOST || (out_keys && res->where != BB_DEVICE))
+      if ((rc = s_sync(s))) return rc;
     return BB_OK;
   }
 
@@ -995,7 +1105,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         (rc = x->ovf.ensure(256)))
       return rc;
     if (!x->ovf_host) BB_HIP(hipHostMalloc((void**)&x->ovf_host, 4, hipHostMallocDefault));
-    BB_HIP(hipMemsetAsync(x->ovf.p, 0, 4, s));
+    if ((rc = s_memset(x->ovf.p, 0, 4, s))) return rc;
   }
 
   for (int64_t b0 = 0; b0 < B; b0 += Bc) {
@@ -1542,12 +1652,14 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     if (out_keys) {  // key lists out: device buffers, or host buffers (copied, synchronised below)
       const hipMemcpyKind kind = res->where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
       for (int side = 0; side < sides; ++side)
-        BB_HIP(hipMemcpyAsync(res->keys + ((size_t)side * B + b0) * K_int, fin_keys + (size_t)side * side_keys,
-                              (size_t)bc * K_int * 8, kind, s));
-      if (drop)
-        BB_HIP(hipMemcpyAsync(res->max_keys + b0, maxk, (size_t)bc * 8, kind, s));
-      else if (res->where == BB_DEVICE)
-        BB_HIP(hipMemsetAsync(res->max_keys + b0, 0, (size_t)bc * 8, s));
+        if ((rc = s_copy(res->keys + ((size_t)side * B + b0) * K_int, fin_keys + (size_t)side * side_keys,
+                         (size_t)bc * K_int * 8, kind, s)))
+          return rc;
+      if (drop) {
+        if ((rc = s_copy(res->max_keys + b0, maxk, (size_t)bc * 8, kind, s))) return rc;
+      } else if (res->where == BB_DEVICE) {
+        if ((rc = s_memset(res->max_keys + b0, 0, (size_t)bc * 8, s))) return rc;
+      }
       else
         memset(res->max_keys + b0, 0, (size_t)bc * 8);
       continue;
@@ -1600,6 +1712,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   if (stream) {
     // a candidate region overflowed (masses of equal scores, a pilot sample unlike the rest):
     // the caller reruns the search on the exact slab path
+    if ((rc = s_sync(s))) return rc;  // (fails a plan before the host copy is recorded)
     BB_HIP(hipMemcpyAsync(x->ovf_host, x->ovf.p, 4, hipMemcpyDeviceToHost, s));
     BB_HIP(hipStreamSynchronize(s));
     if (*x->ovf_host && ab_env("BB_STREAM_DEBUG")) {
@@ -1632,7 +1745,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     BB_HIP(hipMemcpyAsync(res->ids, o_id, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
     if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, o_cnt, (size_t)B * 4, hipMemcpyDeviceToHost, s));
   }
-  if (host_out || where == BB_HOST || (out_keys && res->where != BB_DEVICE)) BB_HIP(hipStreamSynchronize(s));
+  if (host_out || where == BB_HOST || (out_keys && res->where != BB_DEVICE))
+    if ((rc = s_sync(s))) return rc;
   return BB_OK;
 }
 
@@ -1641,7 +1755,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
 extern "C" {
 
 int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
-  if (!x || !q || !res) return fail(BB_E_ARG, "null argument");
+  BB_CHECK_INDEX(x, "bb_search");
+  if (!q || !res) return fail(BB_E_ARG, "bb_search: null argument");
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
   const hipStream_t s = call_stream(x, q);
@@ -1659,7 +1774,8 @@ int bb_search(bb_index* x, const bb_query* q, bb_result* res) {
 
 int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint64_t* max_keys, int32_t n_parts,
                 bb_result* res) {
-  if (!x || !q || !keys || !res || n_parts <= 0) return fail(BB_E_ARG, "bb_finalize: bad arguments");
+  BB_CHECK_INDEX(x, "bb_finalize");
+  if (!q || !keys || !res || n_parts <= 0) return fail(BB_E_ARG, "bb_finalize: bad arguments");
   int32_t sides, K_int;
   int rc = side_k_int(q, &sides, &K_int);
   if (rc) return rc;
@@ -1713,7 +1829,7 @@ int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint
 }
 
 int bb_set_option(bb_index* x, int32_t option, int64_t value) {
-  if (!x) return fail(BB_E_ARG, "null index");
+  BB_CHECK_INDEX(x, "bb_set_option");
   std::lock_guard<std::mutex> lk(x->mu);
   switch (option) {
     case BB_OPT_STREAM:
@@ -1747,13 +1863,14 @@ int bb_set_option(bb_index* x, int32_t option, int64_t value) {
 }
 
 int bb_set_profiling(bb_index* x, int32_t on) {
-  if (!x) return fail(BB_E_ARG, "null index");
+  BB_CHECK_INDEX(x, "bb_set_profiling");
   x->prof = on != 0;
   return BB_OK;
 }
 
 int bb_get_profile(bb_index* x, bb_profile* out) {
-  if (!x || !out) return fail(BB_E_ARG, "null argument");
+  BB_CHECK_INDEX(x, "bb_get_profile");
+  if (!out) return fail(BB_E_ARG, "bb_get_profile: null argument");
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
   for (auto& p : x->pending) {
@@ -1775,6 +1892,93 @@ int bb_get_profile(bb_index* x, bb_profile* out) {
     x->launches[i] = 0;
   }
   return BB_OK;
+}
+
+// ---- prepared searches ----------------------------------------------------------------------
+int bb_plan_create(bb_index* x, const bb_query* q, const bb_result* res, bb_plan** out) {
+  BB_CHECK_INDEX(x, "bb_plan_create");
+  if (!q || !res || !out) return fail(BB_E_ARG, "bb_plan_create: null argument");
+  *out = nullptr;
+  if (q->where != BB_DEVICE || res->where != BB_DEVICE)
+    return fail(BB_E_ARG, "bb_plan_create: a plan reads device query buffers and writes device results");
+  bb_index* root = x->base ? x->base : x;
+  bb_index* v = nullptr;
+  int rc = bb_create_view(root, &v);
+  if (rc) return rc;
+  {
+    std::lock_guard<std::mutex> lk(x->mu);  // the options of the handle the plan is made from
+    v->stream_opt = x->stream_opt;
+    v->stream_min_items = x->stream_min_items;
+    v->refine_opt = x->refine_opt;
+    v->lists_opt = x->lists_opt;
+    v->sq_opt = x->sq_opt;
+    v->ws_cap = x->ws_cap;
+    v->ws_set = x->ws_set;
+  }
+  bb_plan* p = new bb_plan();
+  p->view = v;
+  p->device = v->device;
+  {
+    DeviceGuard g(v->device);
+    p->s = call_stream(v, q);
+    bb_result r2 = *res;
+    tl_capture = &p->ops;
+    rc = search_locked(v, q, &r2, true);
+    tl_capture = nullptr;
+  }
+  if (rc == BB_OK && p->ops.empty()) rc = fail(BB_E_STATE, "bb_plan_create: the search recorded no launches");
+  if (rc) {
+    const std::string msg = g_err;
+    delete p;
+    (void)bb_destroy(v);
+    g_err = msg;
+    return rc == kRetrySlab ? BB_E_STATE : rc;
+  }
+  p->argv.resize(p->ops.size());
+  for (size_t i = 0; i < p->ops.size(); ++i)
+    for (uint32_t o : p->ops[i].offs) p->argv[i].push_back(p->ops[i].blob.data() + o);
+  live_add(p);
+  *out = p;
+  return BB_OK;
+}
+
+int bb_plan_launch(bb_plan* p) {
+  const int rc0 = check_plan(p, "bb_plan_launch");
+  if (rc0) return rc0;
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != p->device) BB_HIP(hipSetDevice(p->device));
+  for (size_t i = 0; i < p->ops.size(); ++i) {
+    const CapturedOp& op = p->ops[i];
+    hipError_t e;
+    if (op.kind == 0)
+      e = hipLaunchKernel(op.func, op.grid, op.block, p->argv[i].data(), op.shmem, p->s);
+    else if (op.kind == 1)
+      e = hipMemsetAsync(op.dst, op.value, op.bytes, p->s);
+    else
+      e = hipMemcpyAsync(op.dst, op.src, op.bytes, hipMemcpyDeviceToDevice, p->s);
+    if (e != hipSuccess) {
+      if (cur >= 0 && cur != p->device) (void)hipSetDevice(cur);
+      return fail(BB_E_HIP, std::string("bb_plan_launch: ") + hipGetErrorString(e));
+    }
+  }
+  if (cur >= 0 && cur != p->device) (void)hipSetDevice(cur);
+  return BB_OK;
+}
+
+int bb_plan_destroy(bb_plan* p) {
+  if (!p) return BB_OK;
+  const int rc0 = check_plan(p, "bb_plan_destroy");
+  if (rc0) return rc0;
+  live_del(p);
+  {
+    DeviceGuard g(p->device);
+    // the replays ran on the caller's stream, which may be gone by now: wait for the device
+    (void)hipDeviceSynchronize();
+  }
+  const int rc = bb_destroy(p->view);
+  p->magic = 0;
+  delete p;
+  return rc;
 }
 
 }  // extern "C"

@@ -5,6 +5,10 @@
 #include <hip/hip_ext.h>
 #include <stdint.h>
 
+#include <cstring>
+#include <type_traits>
+#include <vector>
+
 namespace bb {
 
 // A/B and probe switches (BB_NO_RR, BB_S16, BB_DUAL, BB_SELECT_TRACE, ...): read only when
@@ -68,8 +72,53 @@ struct LaunchProf {
 };
 inline thread_local LaunchProf tl_launch_prof;
 
-template <typename... Args, typename F = void (*)(Args...)>
-inline void bb_launch(F kernel, const dim3& grid, const dim3& block, std::uint32_t shmem, hipStream_t s, Args... args) {
+// Prepared searches (bb_plan_create, api.hip): while a plan is being built, every launch of
+// the search is recorded — kernel, grid, block, LDS bytes and its arguments converted to the
+// kernel's parameter types and packed at their alignments — instead of going out;
+// bb_plan_launch replays the record with hipLaunchKernel, so a repeated request costs its
+// launches and nothing of the host logic that chose and sized them.
+struct CapturedOp {
+  int kind = 0;  // 0 kernel launch, 1 memset, 2 device-to-device copy
+  const void* func = nullptr;
+  dim3 grid, block;
+  std::uint32_t shmem = 0;
+  std::vector<char> blob;          // the arguments, each at its offset
+  std::vector<std::uint32_t> offs;
+  void* dst = nullptr;
+  const void* src = nullptr;
+  std::size_t bytes = 0;
+  int value = 0;
+};
+inline thread_local std::vector<CapturedOp>* tl_capture = nullptr;
+
+template <typename... KArgs>
+inline void capture_launch(const void* f, const dim3& grid, const dim3& block, std::uint32_t shmem, KArgs... a) {
+  CapturedOp op;
+  op.func = f;
+  op.grid = grid;
+  op.block = block;
+  op.shmem = shmem;
+  std::size_t off = 0;
+  auto put = [&](const auto& v) {
+    using T = std::decay_t<decltype(v)>;
+    static_assert(alignof(T) <= 16, "kernel argument alignment");
+    off = (off + alignof(T) - 1) & ~(alignof(T) - 1);
+    op.offs.push_back((std::uint32_t)off);
+    op.blob.resize(off + sizeof(T));
+    std::memcpy(op.blob.data() + off, &v, sizeof(T));
+    off += sizeof(T);
+  };
+  (put(a), ...);
+  tl_capture->push_back(std::move(op));
+}
+
+template <typename... KArgs, typename... Args>
+inline void bb_launch(void (*kernel)(KArgs...), const dim3& grid, const dim3& block, std::uint32_t shmem, hipStream_t s,
+                      Args... args) {
+  if (tl_capture) {
+    capture_launch<KArgs...>((const void*)kernel, grid, block, shmem, static_cast<KArgs>(args)...);
+    return;
+  }
   LaunchProf& p = tl_launch_prof;
   if (p.stop) {
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, p.start, p.stop, 0, args...);

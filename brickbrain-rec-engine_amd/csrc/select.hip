@@ -902,7 +902,9 @@ __device__ __forceinline__ int csw_select(Fetch fetch, int n, uint32_t K, uint64
     if (pages > 1) load(pg);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const bool take = v[j] >= kth;
+      // empty keys (0: padding, a carry list shorter than K) never count: with fewer than K
+      // real keys kth is 0, and a page must still return at most K keys
+      const bool take = v[j] != 0ull && v[j] >= kth;
       const uint64_t bal = __ballot(take);
       const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
       if (take && m + below < (uint32_t)kMaxKInt) sel[m + below] = v[j];

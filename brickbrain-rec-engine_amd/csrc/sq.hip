@@ -252,7 +252,9 @@ __device__ __forceinline__ float sq_row_scale(const float (&v)[kQnC]) {
   if (!(m > 0.f) || !(m <= 3.4e38f)) return 1.f;
   int e;
   (void)frexpf(m, &e);  // m = f·2^e, f in [0.5, 1)
-  return ldexpf(1.f, 14 - e);
+  // at most 2^126 (finite): a row whose largest |q| is below ~2^-112 scales to below 2^14,
+  // still exact (a power of two), its small elements covered by the split's 2^-24 term
+  return ldexpf(1.f, min(14 - e, 126));
 }
 
 __device__ __forceinline__ float sq_margin_row(const SqArgs& a, const float (&v)[kQnC]) {
@@ -488,13 +490,17 @@ __device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* t
   }
   const float margin = sq_margin_row(a, qv);
   uint32_t top;
-  if (kth) {  // the largest multiple of 2^16 with >= K workgroup maxima at or above it
+  if (kth) {  // the largest multiple of 2^16 with >= K list keys at or above it (every key of
+              // every list is a distinct item, so K of them reach it: counting the workgroup
+              // maxima alone left the bound at 0 when fewer than K workgroups hold an item)
     uint32_t prefix = 0;
     for (int bit = 31; bit >= 16; --bit) {
       const uint32_t c = prefix | (1u << bit);
       int cnt = 0;
 #pragma unroll
-      for (int i = 0; i < NL; ++i) cnt += __popcll(__ballot(ordk_of(ent[i][0]) >= c));
+      for (int i = 0; i < NL; ++i)
+#pragma unroll
+        for (int j = 0; j < kSqM; ++j) cnt += __popcll(__ballot(ordk_of(ent[i][j]) >= c));
       if (cnt >= K) prefix = c;
     }
     top = prefix;

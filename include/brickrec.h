@@ -230,7 +230,28 @@ int bb_get_rows(bb_index* idx, const int64_t* ids, int32_t B, void* out, int32_t
  * a view, or to a base while it has views, fail with BB_E_STATE; destroy the views first. */
 int bb_create_view(bb_index* base, bb_index** out);
 
+/* Prepared searches (no reference counterpart: the serving loop's repeated request).  The
+ * reference answers one request per call — get_similar_sets of one target row
+ * (recommendation_system.py:213-217), the retriever's one embedding (lego_nlp_recommeder.py:305)
+ * — and so does a server here: the same query shape with new contents every time.
+ * bb_plan_create runs the host side of bb_search once (path choice, sizes, kernel arguments)
+ * and records its launches instead of issuing them; bb_plan_launch replays them, reading the
+ * query buffers' CURRENT contents and writing the results, at the cost of the launches alone.
+ * q and res must name device buffers (where = BB_DEVICE) that stay allocated while the plan
+ * lives; the plan runs on q->stream (NULL: its own stream; BB_Q_NULL_STREAM: the null stream).
+ * The plan owns a private view of the index (its own workspace): plans never race with
+ * bb_search or with each other on scratch buffers, and the index accepts no upload while a
+ * plan exists (BB_E_STATE, as with views).  Searches that synchronise with the host (the
+ * streaming top-K of indexes >= BB_OPT_STREAM_MIN_ITEMS rows) return BB_E_STATE: use
+ * bb_search for those.  bb_plan_destroy waits for the device before releasing the view. */
+typedef struct bb_plan bb_plan;
+int bb_plan_create(bb_index* idx, const bb_query* q, const bb_result* res, bb_plan** out);
+int bb_plan_launch(bb_plan* plan);
+int bb_plan_destroy(bb_plan* plan);
+
 int bb_info(bb_index* idx, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* r);
+/* Handles are checked by every entry point: a destroyed, foreign or corrupted bb_index /
+ * bb_plan pointer returns BB_E_ARG with a message in bb_last_error(), never a crash. */
 int bb_destroy(bb_index* idx);
 const char* bb_last_error(void);
 int bb_abi_version(void);

@@ -103,3 +103,42 @@ def test_missing_library_is_an_error(monkeypatch):
     monkeypatch.setattr(L, "_lib", None)
     with pytest.raises(L.BrickrecError):
         L.load()
+
+
+def test_stale_and_foreign_handles_are_errors():
+    """every entry point checks its handle against the library's live set
+    before touching it — a pointer the library never made (or one it already destroyed: the
+    r04 segfault class) returns BB_E_ARG with a message instead of crashing the process.  No
+    device is needed: the check comes before any HIP call."""
+    from brickrec import _lib as L
+    lib = L.load()
+    junk = C.create_string_buffer(b"\xab" * 4096)       # bytes that are no bb_index
+    gone = C.create_string_buffer(4096)
+    gone_addr = C.addressof(gone)
+    del gone                                            # freed memory, as after bb_destroy
+    q = L.bb_query(mode=L.BB_MODE_SEMANTIC, B=1, k=10, where=L.BB_DEVICE)
+    res = L.bb_result(where=L.BB_DEVICE)
+    prof = L.bb_profile()
+    n, d = C.c_int64(), C.c_int32()
+    for addr in (C.addressof(junk), gone_addr):
+        h = C.c_void_p(addr)
+        calls = {
+            "bb_search": lambda: lib.bb_search(h, C.byref(q), C.byref(res)),
+            "bb_finalize": lambda: lib.bb_finalize(h, C.byref(q), h, h, 1, C.byref(res)),
+            "bb_info": lambda: lib.bb_info(h, C.byref(n), C.byref(d), None, None),
+            "bb_set_option": lambda: lib.bb_set_option(h, L.BB_OPT_STREAM, 0),
+            "bb_set_profiling": lambda: lib.bb_set_profiling(h, 1),
+            "bb_get_profile": lambda: lib.bb_get_profile(h, C.byref(prof)),
+            "bb_get_rows": lambda: lib.bb_get_rows(h, h, 1, h, L.BB_HOST),
+            "bb_upload_cf": lambda: lib.bb_upload_cf(h, h, 4, L.BB_F32, None),
+            "bb_create_view": lambda: lib.bb_create_view(h, C.byref(C.c_void_p())),
+            "bb_plan_create": lambda: lib.bb_plan_create(h, C.byref(q), C.byref(res), C.byref(C.c_void_p())),
+            "bb_plan_launch": lambda: lib.bb_plan_launch(h),
+            "bb_plan_destroy": lambda: lib.bb_plan_destroy(h),
+            "bb_destroy": lambda: lib.bb_destroy(h),
+        }
+        for name, call in calls.items():
+            assert call() == L.BB_E_ARG, name
+            assert b"stale or foreign" in lib.bb_last_error(), name
+    # NULL stays "nothing to destroy"
+    assert lib.bb_destroy(None) == L.BB_OK and lib.bb_plan_destroy(None) == L.BB_OK

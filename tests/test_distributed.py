@@ -224,6 +224,11 @@ def test_local_bits_rejects_foreign_packed_words():
     assert si._local_bits(np.zeros(W, np.uint32), False).dtype == torch.int32
     assert si._local_bits(np.zeros((3, W), np.uint32), True).shape == (3, W)
     assert si._local_bits(np.ones(100, bool), False).shape == (W,)
+    # plain Python lists: packed like the arrays they stand for
+    assert np.array_equal(si._local_bits([True] * 100, False).numpy(), si._local_bits(np.ones(100, bool), False).numpy())
+    assert si._local_bits([[False] * 100] * 2, True).shape == (2, W)
+    with pytest.raises(ValueError):
+        si._local_bits([True] * 77, False)
     for bad, rows in ((torch.zeros(W + 1, dtype=torch.int32), False), (np.zeros(W * 2, np.uint32), False),
                       (torch.zeros((2, W), dtype=torch.int32), False), (np.zeros(W, np.int32), True),
                       (torch.zeros(W, dtype=torch.int64), False), (np.ones(77, bool), False)):

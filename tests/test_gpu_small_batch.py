@@ -350,3 +350,116 @@ def test_prepared_search_keeps_its_view_alive(c1):
     assert np.array_equal(out[1].cpu().numpy(), ref[1])
     del run
     gc.collect()
+
+
+def _torch_args(dev, **kw):
+    import torch
+    out = {}
+    for k, v in kw.items():
+        if v is None:
+            continue
+        if k in ("mask", "excl"):
+            v = torch.from_numpy(np.asarray(v).view(np.int32) if np.asarray(v).dtype == np.uint32
+                                 else __import__("brickrec").bits_from_bool(v).view(np.int32))
+        else:
+            v = torch.from_numpy(np.ascontiguousarray(v))
+        out[k] = v.to(dev)
+    return out
+
+
+@pytest.mark.parametrize("B", [1, 16, 256])
+def test_plan_replays_the_search(brickrec, B):
+    """prepared_search runs a bb_plan — the host side of the search ran once,
+    each call replays its launches on the inputs' CURRENT contents.  Every mode (semantic,
+    similar with a mask, CF with rated exclusions, hybrid), on the small-batch (B <= 16) and the
+    list (B = 256) paths: the replayed results equal bb_search's bit for bit after the query
+    buffers are rewritten in place between calls."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n, d, r = 25216, 384, 50
+    rng = np.random.default_rng(900 + B)
+    x = R.unit_rows(n, d, 1234)
+    f = rng.normal(0, 0.1, (n, r)).astype(np.float32)
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x, prenormalized=True)
+        idx.upload_cf(f)
+        mask = rng.random(n) < 0.3
+        excl = rng.random((B, n)) < 0.002
+        cases = {"semantic": dict(q_rows=R.unit_rows(B, d, 5)),
+                 "similar": dict(q_items=rng.choice(n, B, replace=False).astype(np.int64), mask=mask),
+                 "cf": dict(q_cf=rng.normal(0, 0.1, (B, r)).astype(np.float32), excl=excl),
+                 "hybrid": dict(q_items=rng.choice(n, B, replace=False).astype(np.int64),
+                                q_cf=rng.normal(0, 0.1, (B, r)).astype(np.float32), mask=mask, excl=excl)}
+        for mode, kw in cases.items():
+            k = 10
+            targs = _torch_args(dev, **kw)
+            run, out = idx.prepared_search(mode, k, **targs)
+            assert type(run).__name__ == "_Plan", type(run)
+            for rep in range(3):
+                if rep:   # new request contents in the same buffers
+                    if "q_rows" in kw:
+                        kw["q_rows"] = R.unit_rows(B, d, 50 + rep)
+                    if "q_items" in kw:
+                        kw["q_items"] = rng.choice(n, B, replace=False).astype(np.int64)
+                    if "q_cf" in kw:
+                        kw["q_cf"] = rng.normal(0, 0.1, (B, r)).astype(np.float32)
+                    for key in ("q_rows", "q_items", "q_cf"):
+                        if key in kw:
+                            targs[key].copy_(torch.from_numpy(kw[key]).to(dev))
+                run()
+                torch.cuda.synchronize()
+                ref = idx.search(mode, k, **kw)
+                assert np.array_equal(out[2].cpu().numpy(), ref[2]), (mode, rep)
+                assert np.array_equal(out[1].cpu().numpy(), ref[1]), (mode, rep)
+                assert np.array_equal(out[0].cpu().numpy().view(np.uint32), ref[0].view(np.uint32)), (mode, rep)
+            # while the plan lives the index takes no upload (its private view reads the rows)
+            with pytest.raises(brickrec.BrickrecError):
+                idx.upload_cf(f)
+            run.close()
+        idx.upload_cf(f)   # every plan closed: uploads work again
+    finally:
+        idx.close()
+
+
+def test_plan_refused_on_streaming_falls_back(brickrec):
+    """A streaming search reads its overflow flag on the host: bb_plan_create refuses it
+    (BB_E_STATE) and prepared_search keeps the bb_search call — same results."""
+    import torch
+    n, d, B, k = 3000, 128, 8, 10
+    x = R.unit_rows(n, d, 31)
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x)
+        idx.set_option("stream", 1)
+        q = torch.from_numpy(R.unit_rows(B, d, 32)).cuda()
+        run, out = idx.prepared_search("semantic", k, q_rows=q)
+        assert type(run).__name__ != "_Plan"
+        run()
+        torch.cuda.synchronize()
+        ref = idx.search("semantic", k, q_rows=q.cpu().numpy())
+        assert np.array_equal(out[1].cpu().numpy(), ref[1])
+    finally:
+        idx.close()
+
+
+def test_destroyed_handle_is_an_error(brickrec):
+    """VERDICT r04 item 6 on the device: a handle already passed to bb_destroy (the r04r
+    use-after-free) returns BB_E_ARG from bb_search, and a closed plan from bb_plan_launch."""
+    import ctypes as C
+    import torch
+    from brickrec import _lib as L
+    lib = L.load()
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(R.unit_rows(1000, 64, 3))
+    q = torch.from_numpy(R.unit_rows(2, 64, 4)).cuda()
+    run, out = idx.prepared_search("semantic", 5, q_rows=q)
+    p = run._p
+    h = C.c_void_p(idx._h.value)
+    idx.close()          # closes the plan first, then the index
+    assert lib.bb_plan_launch(p) == L.BB_E_ARG
+    qs = L.bb_query(mode=L.BB_MODE_SEMANTIC, B=2, k=5, where=L.BB_DEVICE, q_rows=q.data_ptr())
+    res = L.bb_result(scores=out[0].data_ptr(), ids=out[1].data_ptr(), where=L.BB_DEVICE)
+    assert lib.bb_search(h, C.byref(qs), C.byref(res)) == L.BB_E_ARG
+    assert b"stale or foreign" in lib.bb_last_error()
+    assert lib.bb_destroy(h) == L.BB_E_ARG

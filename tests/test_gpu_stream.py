@@ -322,3 +322,40 @@ def test_stream_small_pilot_pages(brickrec):
     (sc, ids, cnt), slab = _both(idx, "semantic", k, stream_gemms=2, q_rows=q)
     _same((sc, ids, cnt), slab)
     assert np.all(cnt == k)
+
+
+def test_stream_refine_short_carry_paged(brickrec):
+    """Two-level bound where a selective mask leaves pass A's list (the carry) with fewer than
+    K real keys, and pass B more than 2,048 candidates: the final candidate select pages
+    (1,024 keys) and its last page holds more than K keys but fewer than K real ones (the
+    carry's empty keys at its end).  Each page must return at most K keys (the
+    page's K-th key was 0 there and every slot was taken, past the wave's LDS list)."""
+    n, d, B, k = 200000, 384, 64, 50
+    x = R.unit_rows(n, d, 81)
+    q = R.unit_rows(B, d, 82)
+    mask = np.zeros(n, bool)
+    mask[np.arange(10) * 97] = True                                  # pass A: 10 eligible
+    mask[np.linspace(100000, n - 1, 2068).astype(np.int64)] = True   # pass B: 2,068
+    idx = brickrec.ItemIndex(dtype="bf16")
+    idx.upload_items(x)
+    idx.set_option("workspace_bytes", 2 << 20)   # pilot 8,192 rows: n1 ~ 40K < 100K
+    idx.set_option("stream_refine", 1)
+    idx.set_option("stream", 1)
+    idx.set_profiling(True)
+    a = idx.search("semantic", k, q_rows=q, mask=mask)
+    prof = idx.profile()
+    idx.set_profiling(False)
+    assert prof["rerun"]["launches"] == 0, prof
+    assert prof["gemm"]["launches"] == 3, prof
+    idx.set_option("stream", 0)
+    b = idx.search("semantic", k, q_rows=q, mask=mask)
+    _same(a, b)
+    sc, ids, cnt = a
+    assert np.all(cnt == k)
+    rows = idx.get_rows(np.arange(n)).astype(np.float64)
+    sim = R.normalize_rows(q).astype(np.float64) @ rows.T
+    for i in range(0, B, 8):
+        assert mask[ids[i]].all() and len(set(ids[i])) == k
+        ri, rs = R.topk_indices(sim[i], k, mask)
+        # bf16 query operand vs the f32 query here: ~1e-3 apart
+        np.testing.assert_allclose(sc[i], rs, atol=5e-3, rtol=0)
