@@ -9,9 +9,11 @@ name); this module restates the row order, the text and the metadata, so that an
 file (``indexfile.write_index(..., documents=...)``) records which document each embedding
 row is and a later encoder run can be lined up with it.
 
-Parity is UNPINNED: the module that holds these functions does not import here (langchain
-and sentence-transformers are absent), so no golden output of the reference
-exists.  Two choices the SQL leaves open are fixed here and documented: rows tied on
+Parity is pinned by ``tests/golden/g6_documents.json``: the module that holds these functions
+does not import here (langchain and sentence-transformers are absent), so
+``oracle/gen_documents.py`` runs the reference's own three pieces of code (taken out of its
+syntax tree) and its SQL on a synthetic catalogue, and ``tests/test_documents.py`` compares
+every sampled row.  Two choices the SQL leaves open are fixed here and documented: rows tied on
 (num_parts, year) keep their input order (set_num ascending from ``document_rows``), and
 ``STRING_AGG(DISTINCT cat.name, ', ')`` lists the categories in ascending order (what
 Postgres' sort-based DISTINCT produces).

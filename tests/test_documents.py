@@ -2,9 +2,15 @@
 _create_set_description / _estimate_complexity (lego_nlp_recommeder.py:196-267, 372-427),
 restated in brickrec/documents.py, recorded beside the rows in the index file.
 
-Parity UNPINNED: lego_nlp_recommeder.py does not import here (langchain / sentence-
-transformers absent), so no golden output of the reference exists.  The expected
-strings below are written out by hand from the reference's f-strings (:382-408)."""
+Parity PINNED (round 5): tests/golden/g6_documents.json holds what the reference's own code
+produced — oracle/gen_documents.py takes _create_set_description, _estimate_complexity and
+prep_vectorDB's document loop out of the module's syntax tree (the module itself does not
+import: langchain / sentence-transformers are absent) and runs them, with the
+reference's document SQL, on a synthetic sqlite catalogue.  The hand-written cases below keep
+the NULL-count edge (a NaN colour count), which Postgres' COUNT never produces."""
+import json
+import os
+
 import numpy as np
 
 from brickrec.documents import build_documents, create_set_description, estimate_complexity, order_rows
@@ -56,3 +62,35 @@ def test_row_order_and_index_file(tmp_path):
     assert f.set_nums == names and f.descriptions == desc and f.metadata == meta
     np.testing.assert_array_equal(np.asarray(f.rows), x)
     assert build_documents(ROWS, limit=2)[0] == ["10294-1", "75192-1"]
+
+
+G6 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "g6_documents.json")
+
+
+def test_documents_match_the_reference_golden():
+    """Every sampled row of the reference's document query: the restated description, metadata
+    and complexity equal what the reference's code produced from the same row."""
+    from brickrec.documents import document_metadata
+    g = json.load(open(G6))
+    assert len(g["rows"]) == len(g["descriptions"]) == len(g["metadata"]) > 300
+    for row, desc, meta in zip(g["rows"], g["descriptions"], g["metadata"]):
+        assert create_set_description(row) == desc, row["set_num"]
+        assert document_metadata(row) == meta, row["set_num"]
+        assert estimate_complexity(row) == meta["complexity"]
+
+
+def test_row_order_matches_the_reference_golden():
+    """ORDER BY num_parts DESC, year DESC (the reference's SQL, run by the generator): the
+    restated order of the same rows, given in any order, is the reference's up to rows tied
+    on both keys (whose order the SQL leaves open)."""
+    g = json.load(open(G6))
+    rows = g["rows"]
+    perm = np.random.default_rng(5).permutation(len(rows))
+    ordered = order_rows([rows[i] for i in perm])
+    key = lambda r: (r["num_parts"], r["year"])
+    assert [key(r) for r in ordered] == [key(r) for r in rows]
+    groups = {}
+    for r in rows:
+        groups.setdefault(key(r), set()).add(r["set_num"])
+    for r in ordered:
+        assert r["set_num"] in groups[key(r)]
