@@ -1,8 +1,8 @@
-// scan4.hip — launcher of the 64-queries-per-wave bf16 scan (scan4_kernel.h); its own
-// translation unit so the template instances compile in parallel with gemm.hip.
+// scan4.hip — launcher of the 64-queries-per-wave bf16 scan (scan4_kernel.h): shape rules, the
+// hybrid dual-scan instances, and dispatch to the per-width instance units (scan4_launch.h).
 #include <cstdlib>
 
-#include "scan4_kernel.h"
+#include "scan4_launch.h"
 
 namespace bb {
 
@@ -23,36 +23,6 @@ bool scan4_used(int dtype, int Mpad) {
 int scan_chunks(int dtype, int Mpad, int tiles, bool split, int list_ku) {
   if (split || !scan4_used(dtype, Mpad)) return scan_n_chunks(Mpad, tiles);
   return list_ku > 0 ? scan4_list_chunks(Mpad, tiles, list_ku) : scan4_n_chunks(Mpad, tiles);
-}
-
-template <int KU>
-static void launch_t(const GemmArgs& a, hipStream_t s) {
-  const int tiles = a.Ncols / 32;
-  const int n_chunks = a.lists ? scan4_list_chunks(a.Mpad, tiles, KU) : scan4_n_chunks(a.Mpad, tiles);
-  const int blocks = a.Mpad / kScan4Queries * n_chunks;
-  if constexpr (KU <= kRrMaxD / 8) {
-    // the exact re-rank path: the f16 copy of an f32 index
-    if (a.lists) {  // bounded candidate lists
-      bb_launch((scan4_kernel<KU, kScanList | kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a,
-                         n_chunks, tiles);
-      return;
-    }
-    if (a.s_h && !a.cand) {  // int16 score image
-      bb_launch((scan4_kernel<KU, kScanS16 | kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a,
-                         n_chunks, tiles);
-      return;
-    }
-    if (a.f16) {  // f32 score slab
-      bb_launch((scan4_kernel<KU, kScanF16>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
-      return;
-    }
-  }
-  if (a.cand)
-    bb_launch((scan4_kernel<KU, kScanStream>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
-  else if (a.pilot_top)  // streaming pilot: top-m half-tile maxima, no image
-    bb_launch((scan4_kernel<KU, kScanPilot>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
-  else
-    bb_launch((scan4_kernel<KU>), dim3(blocks), dim3(kScanWaves * 64), 0, s, a, n_chunks, tiles);
 }
 
 // The hybrid's two re-rank scans (int16 image) in one launch: content rows of 192..512
@@ -104,16 +74,12 @@ hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t
 int scan4_pilot_m(int kpad) { return kpad * 2 / 16 <= 64 ? 8 : 4; }
 
 bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s) {
-  switch (ku) {
-    case 8: launch_t<8>(a, s); return true;
-    case 16: launch_t<16>(a, s); return true;
-    case 24: launch_t<24>(a, s); return true;
-    case 32: launch_t<32>(a, s); return true;
-    case 48: launch_t<48>(a, s); return true;
-    case 64: launch_t<64>(a, s); return true;
-    case 96: launch_t<96>(a, s); return true;
-    default: return false;
+  if (ku <= kRrMaxD / 8) {  // the exact re-rank path first (the f16 copy of an f32 index)
+    bool launched = false;
+    if ((launch_scan4_rr_lo(a, ku, s, launched) || launch_scan4_rr_hi(a, ku, s, launched)) && launched) return true;
   }
+  return launch_scan4_bf_lo(a, ku, s) || launch_scan4_bf_48(a, ku, s) || launch_scan4_bf_64(a, ku, s) ||
+         launch_scan4_bf_96(a, ku, s);
 }
 
 }  // namespace bb

@@ -574,9 +574,33 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     // and both blocks' epilogues of tile t-1 are woven into tile t, after its DMA pieces.
     f32x16s accA1 = {}, accB1 = {};
     uint32_t pewA = 0;
-    auto il_body = [&](auto BUF, auto EPI, int tile) __attribute__((always_inline)) {
+    // Sparse list epilogue (masks: configs[2]'s ~2 % dense constraint mask).  The mask and the
+    // item space are per item, so whether accumulator register g can hold an eligible item is
+    // the same for every lane of a half: u = the union over both halves (uniform).  When u has
+    // at most kSparseRegs registers, the list epilogue of the previous tile inserts only those
+    // (a scalar loop, the register picked by a uniform index) instead of all sixteen register
+    // pairs — the masked-out ones would insert code 0, a no-op.  The lists are the same keys.
+    auto list_sparse = [&](const f32x16s& p, int ptile, uint32_t eew, float k2, ListTop5& L, ListTop2& R,
+                           uint32_t u) __attribute__((always_inline)) {
+      const int ptile0 = ptile * 32;
+      const uint32_t e16 = list_elig16(ppw & pmw & ~eew, ptile0, a.n_valid, h);
+      const uint32_t pb = (uint32_t)l_cnt << 4;
+      for (uint32_t uu = u; uu; uu &= uu - 1u) {
+        const int g = __builtin_ctz(uu);
+        const float v = p[g];
+        const uint32_t c =
+            __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_u16(fmaf(v, k2, 0.5f), 0.f)) & 0xFFFFu;
+        L.ins(((e16 >> g) & 1u) ? (c << 16) | pb | (uint32_t)g : 0u);
+      }
+      if (a.r0lists) {
+        const float m = list_present_max(p, list_elig16(ppw, ptile0, a.n_valid, h));
+        R.ins(list_r0_key(m, k2, (uint32_t)(ptile - tile_lo)));
+      }
+    };
+    auto il_body = [&](auto BUF, auto EPI, auto SPC, int tile, uint32_t su) __attribute__((always_inline)) {
       constexpr int buf = decltype(BUF)::value;
       constexpr bool epi = decltype(EPI)::value;
+      constexpr bool SP = decltype(SPC)::value;  // sparse list epilogue (registers su only)
       f32x16s& cA = buf ? accA1 : accA;
       f32x16s& cB = buf ? accB1 : accB;
       f32x16s& pA = buf ? accA : accA1;  // the previous tile's set
@@ -619,7 +643,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
           // steps from 2), the next tile's words, then the previous tile's list epilogue of
           // block A and block B (odd steps between the pieces, then one per step) and the
           // period counter
-          constexpr int kE = 2 * kLE + 1;
+          constexpr int kE = SP ? 3 : 2 * kLE + 1;
           static_for<PIECES + 2 + kE>([&](auto SL) {
             constexpr int s = decltype(SL)::value;
             constexpr int e = s - PIECES - 2;  // epilogue slice index (s >= PIECES + 2)
@@ -640,10 +664,13 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
                 nw_eA = erowA[w0 + wtile];
                 nw_eB = erowB[w0 + wtile];
               } else if constexpr (epi) {
-                if constexpr (e < kLE) {
+                if constexpr (SP && e < 2) {
+                  if constexpr (e == 0) list_sparse(pA, tile - 1, pewA, k2A, lstA, r0A, su);
+                  else list_sparse(pB, tile - 1, pewB, k2B, lstB, r0B, su);
+                } else if constexpr (!SP && e < kLE) {
                   list_slice(std::integral_constant<int, e>{}, pA, tile - 1, ppw, pmw, pewA, k2A, lstA, r0A, le16A, lfullA,
                              lkoA);
-                } else if constexpr (e < 2 * kLE) {
+                } else if constexpr (!SP && e < 2 * kLE) {
                   list_slice(std::integral_constant<int, e - kLE>{}, pB, tile - 1, ppw, pmw, pewB, k2B, lstB, r0B, le16B,
                              lfullB, lkoB);
                 } else {
@@ -704,14 +731,32 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       ewB = nw_eB;
       asm volatile("" : "+v"(pw), "+v"(mw), "+v"(ewA), "+v"(ewB));
     };
-    il_body(B0{}, EN{}, tile_lo);
+    using SN = std::integral_constant<bool, false>;
+    using SY = std::integral_constant<bool, true>;
+    // one tile with the previous tile's epilogue: sparse when at most kSparseRegs registers can
+    // hold an eligible item of it (one uniform branch per tile, decided on the item words)
+    constexpr int kSparseRegs = 8;
+    auto il_step = [&](auto BUF, int tile) __attribute__((always_inline)) {
+      if constexpr (LIST) {
+        const uint32_t w = __builtin_amdgcn_readfirstlane(ppw & pmw);
+        const int pt0 = (tile - 1) * 32;
+        const uint32_t u = list_elig16(w, pt0, a.n_valid, 0) | list_elig16(w, pt0, a.n_valid, 1);
+        if (__builtin_popcount(u) <= kSparseRegs)
+          il_body(BUF, EY{}, SY{}, tile, u);
+        else
+          il_body(BUF, EY{}, SN{}, tile, 0u);
+      } else {
+        il_body(BUF, EY{}, SN{}, tile, 0u);
+      }
+    };
+    il_body(B0{}, EN{}, SN{}, tile_lo, 0u);
     int tile = tile_lo + 1;
     for (;;) {
       if (tile >= tile_hi) break;
-      il_body(B1{}, EY{}, tile);
+      il_step(B1{}, tile);
       ++tile;
       if (tile >= tile_hi) break;
-      il_body(B0{}, EY{}, tile);
+      il_step(B0{}, tile);
       ++tile;
     }
     // both blocks' epilogues of the last tile (not overlapped)

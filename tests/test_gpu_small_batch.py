@@ -426,7 +426,7 @@ def test_plan_refused_on_streaming_falls_back(brickrec):
     """A streaming search reads its overflow flag on the host: bb_plan_create refuses it
     (BB_E_STATE) and prepared_search keeps the bb_search call — same results."""
     import torch
-    n, d, B, k = 3000, 128, 8, 10
+    n, d, B, k = 3000, 128, 40, 10      # B > 16: not the small-batch path
     x = R.unit_rows(n, d, 31)
     idx = brickrec.ItemIndex(dtype="f32")
     try:
