@@ -376,10 +376,24 @@ def run_sharded(args, rank, world, local, dev):
         "kernels_us_per_step": {kk: round(1e3 * v["ms"] / ps, 2) for kk, v in prof.items() if v["launches"]},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        def get_chunk(a, b):
-            return sh.local.get_rows(torch.arange(a, b, device=dev)).float().cpu().numpy()
-        out["cpu_baseline"] = cpu_full_scan(get_chunk, n_loc, q[:64].cpu().numpy(), k)
+    if rank == 0 and not args.no_cpu:
+        # the CPU baseline scans the WHOLE index at every N: rank 0's own
+        # stored rows, and every other rank's shard regenerated as that rank made it (same
+        # seed, rounded to bf16 as stored)
+        from brickrec.distributed import shard_bounds
+        def shard_rows(r):
+            lo_r, hi_r = shard_bounds(n, world, r)
+            if r == rank:
+                return lambda a, b: sh.local.get_rows(torch.arange(a - lo_r, b - lo_r, device=dev)).float().cpu().numpy()
+            xr = unit_rows_torch(hi_r - lo_r, d, 1234 + r, dev).to(torch.bfloat16).float().cpu().numpy()
+            return lambda a, b: xr[a - lo_r:b - lo_r]
+        owners = [(shard_bounds(n, world, r), shard_rows(r)) for r in range(world)]
+
+        def get_chunk(a, b):   # global rows [a, b), possibly spanning shards
+            parts = [f(max(a, lo_r), min(b, hi_r)) for (lo_r, hi_r), f in owners if max(a, lo_r) < min(b, hi_r)]
+            return np.concatenate(parts, 0)
+        out["cpu_baseline"] = cpu_full_scan(get_chunk, n, q[:64].cpu().numpy(), k)
+        del owners
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
@@ -547,18 +561,32 @@ def dry_run(args):
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    sharded = args.workload in SHARDED
     out = {"metric": "similarity queries/sec + p50 latency, 384-d x 25,216 items (configs[1])", "value": None,
            "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
-           "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-           "dtype": args.dtype, "data": "synthetic", "max_rank_s": float(t.item()),
-           "config": {"workload": "dry run (no device)", "parallelism": f"replicas x{world}" if world > 1 else "single"},
+           "ms_per_step": None, "higher_is_better": True, "scaling": "strong" if sharded else "weak",
+           "vs_baseline": None, "dtype": args.dtype, "data": "synthetic", "max_rank_s": float(t.item()),
+           "config": {"workload": f"dry run (no device) of {args.workload}",
+                      "parallelism": (f"rows sharded x{world}" if sharded else f"replicas x{world}") if world > 1
+                      else "single"},
            "roofline": None, "cpu_baseline": None}
     if rank == 0 and not args.no_cpu:
         from oracle.restatement import unit_rows
-        x_np = unit_rows(4096, DIM, 1234)
-        q_np = unit_rows(BATCH, DIM, 4321)
-        out["cpu_baseline"], _ = cpu_baseline(x_np, q_np, TOPK, budget_s=args.cpu_budget, sweep_s=0.0)
-        out["cpu_baseline"]["sample"] += " (dry run: 4,096 rows)"
+        if sharded:   # the sharded CPU leg (cpu_full_scan over every rank's rows), on a small index
+            from brickrec.distributed import shard_bounds
+            c = SHARDED[args.workload]
+            n_dry = 8192
+            shards = [unit_rows(hi - lo, c["d"], 1234 + r) for r, (lo, hi) in
+                      enumerate(shard_bounds(n_dry, world, r) for r in range(world))]
+            full = np.concatenate(shards, 0)
+            out["cpu_baseline"] = cpu_full_scan(lambda a, b: full[a:b], n_dry, unit_rows(64, c["d"], 4321), c["k"],
+                                                budget_s=args.cpu_budget, chunk=4096)
+            out["cpu_baseline"]["sample"] += f" (dry run: {n_dry:,} rows in {world} shards)"
+        else:
+            x_np = unit_rows(4096, DIM, 1234)
+            q_np = unit_rows(BATCH, DIM, 4321)
+            out["cpu_baseline"], _ = cpu_baseline(x_np, q_np, TOPK, budget_s=args.cpu_budget, sweep_s=0.0)
+            out["cpu_baseline"]["sample"] += " (dry run: 4,096 rows)"
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

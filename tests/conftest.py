@@ -23,3 +23,17 @@ def golden():
     def load(name):
         return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
     return load
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Near-tie gate counts of every parity test that ran (tests/_parity.py RECORDS) ->
+    gpurun_out/parity_gates.json (BB_GATE_OUT overrides), so a -q run keeps them."""
+    mod = sys.modules.get("_parity")
+    recs = getattr(mod, "RECORDS", None)
+    if not recs:
+        return
+    import json
+    out = os.environ.get("BB_GATE_OUT", os.path.join(ROOT, "gpurun_out", "parity_gates.json"))
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump({"exitstatus": int(exitstatus), "gates": recs}, f, indent=1)

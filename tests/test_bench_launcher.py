@@ -36,3 +36,21 @@ def test_single_rank_dry_run():
     assert p.returncode == 0, p.stderr[-2000:]
     d = _line(p.stdout)
     assert d["n_gpus"] == 1 and d["cpu_baseline"] is None
+
+
+def test_gpus2_sharded_c5_line_carries_cpu_baseline():
+    """a two-rank sharded line (configs[4], --workload c5) carries the
+    CPU baseline too — rank 0 scans every rank's rows on the host (the dry run: a small index
+    in two shards)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--workload", "c5",
+                        "--steps", "3", "--warmup", "1", "--cpu-budget", "0.3"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _line(p.stdout)
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["parallelism"] == "rows sharded x2"
+    cb = d["cpu_baseline"]
+    assert cb and cb["value"] > 0 and "2 shards" in cb["sample"]

@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 from oracle import restatement as R
-from _parity import GAP, TOL, Gate, check_row
+from _parity import GAP, TOL, Gate, blend_sure, check_row
 
 pytestmark = pytest.mark.gpu
 N25, D25 = 25216, 384
@@ -96,22 +96,32 @@ def test_c2_hybrid_mask_b1024(brickrec, items25):
     sim_c = (xn[liked] @ xn.T).astype(np.float64)
     sim_f = u @ f.T
     gate = Gate("configs[2] hybrid B=1024 + mask")
+    n_sure = 0
     for b in range(B):
         okc = mask.copy()
         okc[R.rank0(sim_c[b])] = False
-        ci, cs = R.topk_indices(sim_c[b], ks + 1, okc)
+        ci, cs = R.topk_indices(sim_c[b], ks + 8, okc)
         okf = mask & ~rated[b]
-        fi, fs = R.topk_indices(sim_f[b], ks + 1, okf)
+        fi, fs = R.topk_indices(sim_f[b], ks + 8, okf)
         hi, hs = R.union_blend(ci[:ks], cs[:ks], fi[:ks], fs[:ks], 0.4, 0.6, k + 1)
         # the union's membership depends on both side boundaries: gate on all three
         side_tie = (len(ci) > ks and cs[ks - 1] - cs[ks] <= GAP) or (len(fi) > ks and fs[ks - 1] - fs[ks] <= GAP)
         L = min(k, len(hi))
-        if side_tie:   # union membership itself is undetermined: lists only need to be ordered
+        if side_tie:
+            # a near-tied side boundary leaves some union memberships open: every blended item
+            # whose membership does not depend on it must still be in the list, with its score
             gate.gated += 1
             assert np.all(np.diff(sc[b][:cnt[b]]) <= 0)
+            sure = blend_sure(ci, cs, fi, fs, ks, 0.4, 0.6, k)
+            got = {int(i): float(s) for i, s in zip(ids[b][:cnt[b]], sc[b][:cnt[b]])}
+            assert set(sure) <= set(got), (b, sorted(set(sure) - set(got)))
+            for i, h in sure.items():
+                assert abs(got[i] - h) <= TOL, (b, i, got[i], h)
+            n_sure += len(sure)
             continue
         check_row(gate, sc[b], ids[b], hi[:L], hs[:L], k, hs[k] if len(hi) > k else None)
         assert cnt[b] == L
+    print(f"[parity] configs[2] gated queries: {n_sure} blended items checked for membership")
     gate.report(0.05)
 
 
@@ -285,6 +295,11 @@ def test_sharded_hybrid_streaming_vs_unsharded_and_oracle(brickrec):
         if cs[2 * k - 1] - cs[2 * k] <= GAP or fs[2 * k - 1] - fs[2 * k] <= GAP:
             gate.gated += 1
             assert np.all(np.diff(sc[b]) <= 0)
+            ci, cs = R.topk_indices(sim, 2 * k + 8, okc)
+            fi, fs = R.topk_indices(fsc, 2 * k + 8, mask & ~excl[b])
+            got = {int(i): float(s) for i, s in zip(ids[b], sc[b]) if i >= 0}
+            for i, h in blend_sure(ci, cs, fi, fs, 2 * k, 0.4, 0.6, k).items():
+                assert i in got and abs(got[i] - h) <= TOL, (b, i)
             continue
         check_row(gate, sc[b], ids[b], hi_[:k], hs[:k], k, hs[k])
     gate.report(0.1)

@@ -107,3 +107,35 @@ def test_constraint_helpers():
     assert create_size_constraints("huge") == []
     h = HardConstraint(ConstraintType.PIECES_MAX, 10)
     assert h.description == "pieces_max: 10"
+
+
+def test_blend_sure_is_sound_and_tight():
+    """tests/_parity.blend_sure (the configs[2] near-tie membership check): with clear side
+    boundaries it names the oracle's whole blended top-k (minus final-boundary near-ties);
+    with a side boundary forced into a tie it names only items whose membership cannot change,
+    and each of those is in the blend under either resolution of the tie."""
+    import numpy as np
+    from oracle import restatement as R
+    from _parity import blend_sure
+    rng = np.random.default_rng(3)
+    for trial in range(40):
+        n, ks, k = 400, 20, 10
+        c = rng.normal(0, 1, n)
+        f = rng.normal(0, 1, n)
+        if trial % 2:          # force a near-tie at the content boundary
+            o = np.argsort(-c)
+            c[o[ks]] = c[o[ks - 1]] - 1e-7
+        ci, cs = R.topk_indices(c, ks + 8)
+        fi, fs = R.topk_indices(f, ks + 8)
+        sure = blend_sure(ci, cs, fi, fs, ks, 0.4, 0.6, k)
+        # both resolutions of a content-boundary tie: the ks-th or the (ks+1)-th item in the list
+        for swap in ((False, True) if trial % 2 else (False,)):
+            cl, csl = list(ci[:ks]), list(cs[:ks])
+            if swap:
+                cl[-1], csl[-1] = ci[ks], cs[ks]
+            hi, hs = R.union_blend(cl, csl, fi[:ks], fs[:ks], 0.4, 0.6, k)
+            got = dict(zip(hi.tolist(), hs.tolist()))
+            for i, h in sure.items():
+                assert i in got and abs(got[i] - h) < 1e-12
+        if trial % 2 == 0:
+            assert len(sure) >= k - 2
