@@ -1499,7 +1499,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
             sa.rr_q_raw_ld = x->d;
             sa.rr_q_raw_d = x->d;
           }
-          static const int ls_ablate = ab_env("BB_LS_ABLATE") ? atoi(ab_env("BB_LS_ABLATE")) : 0;
+          // BB_LS_ABLATE (probe runs) bit 0: one cache-resident rescore row; BB_LS_BITWISE (A/B
+          // runs): the bitwise K-th code search instead of the two-level histogram (ablate bit 2)
+          static const int ls_ablate = (ab_env("BB_LS_ABLATE") ? atoi(ab_env("BB_LS_ABLATE")) : 0) |
+                                       (ab_env("BB_LS_BITWISE") ? 4 : 0);
           sa.ablate = ls_ablate;
           final_pp = pp;
           if (q->mode == BB_MODE_HYBRID && side == 0 && list_f) {

@@ -158,8 +158,11 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   static_assert(KU % 8 == 0, "KU must split into whole 1 KiB pieces per wave");
   constexpr bool STREAM = (ABL & kScanStream) != 0;
   constexpr bool F16 = (ABL & kScanF16) != 0;  // f16 operands: the re-rank copy of an f32 index
-  // item tile ring, + (streaming) a 4-KiB register parking area per wave for the appends
-  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_B + (STREAM ? kScanWaves * 4096 : 0)];
+  // item tile ring — three tiles deep on the interleaved schedule (two tiles of LDS-DMA in flight
+  // while one is read: the ring the MALL / L2 latency needs at one workgroup per CU), two on the
+  // chained d = 768 one (no LDS left) — + (streaming) a 4-KiB register parking area per wave
+  constexpr int RING = IL ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) char smem[RING * TILE_B + (STREAM ? kScanWaves * 4096 : 0)];
 
   const int n_groups = a.Mpad / kScan4Queries;
   const int total = n_groups * n_chunks;
@@ -208,9 +211,14 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory");
   };
 
-  // first tile in flight before the query loads
+  // first tile(s) in flight before the query loads
 #pragma unroll
   for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
+  if constexpr (RING == 3) {
+    const int t1 = tile_lo + 1 < tile_hi ? tile_lo + 1 : tile_lo;  // branch-free staging target
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) stage_piece(t1, 1, p);
+  }
 
   // queries: block A (qA), block B (qB); register j = b·U + u lives in an AGPR iff j < NA
   u32x4v qv[2 * U];
@@ -263,7 +271,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   const size_t w0 = (size_t)(a.slab_start >> 5);
   const uint32_t* erowA = a.excl + (size_t)(qA < a.M_valid ? qA : a.M_valid - 1) * a.excl_ld;
   const uint32_t* erowB = a.excl + (size_t)(qB < a.M_valid ? qB : a.M_valid - 1) * a.excl_ld;
-  float* park = (float*)(smem + 2 * TILE_B) + wave * 1024;
+  float* park = (float*)(smem + RING * TILE_B) + wave * 1024;
   // int16 score image (kScanS16): code scales 1/(h·32767) of the two query blocks
   constexpr bool S16 = (ABL & kScanS16) != 0 && !STREAM;
   float skA = 0.f, skB = 0.f;
@@ -597,20 +605,25 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
         R.ins(list_r0_key(m, k2, (uint32_t)(ptile - tile_lo)));
       }
     };
-    auto il_body = [&](auto BUF, auto EPI, auto SPC, int tile, uint32_t su) __attribute__((always_inline)) {
-      constexpr int buf = decltype(BUF)::value;
+    auto il_body = [&](auto BUF, auto EPI, auto SPC, int tile, uint32_t su, int slot) __attribute__((always_inline)) {
+      constexpr int buf = decltype(BUF)::value;  // accumulator set (tile parity); LDS ring slot: `slot`
       constexpr bool epi = decltype(EPI)::value;
       constexpr bool SP = decltype(SPC)::value;  // sparse list epilogue (registers su only)
       f32x16s& cA = buf ? accA1 : accA;
       f32x16s& cB = buf ? accB1 : accB;
       f32x16s& pA = buf ? accA : accA1;  // the previous tile's set
       f32x16s& pB = buf ? accB : accB1;
-      const int stile = tile + 1 < tile_hi ? tile + 1 : tile;
-      const int wtile = stile;
+      // staging runs two tiles ahead (ring slot slot - 1 mod 3, read by tile - 1, free since the
+      // last barrier); the words of the next tile go out first, so the end-of-tile wait can leave
+      // the youngest tile's DMA in flight
+      const int stile = tile + 2 < tile_hi ? tile + 2 : tile;
+      const int sslot = slot == 0 ? 2 : slot - 1;
+      const int wtile = tile + 1 < tile_hi ? tile + 1 : tile;
+      const char* fbase = smem + slot * TILE_B + rrow;
       auto frag = [&](int u) __attribute__((always_inline)) {
         int sw = swz;
         asm volatile("" : "+v"(sw));
-        return *(const u32x4v*)(smem + buf * TILE_B + rrow + (((2 * (u % G) + h) ^ sw) << 4) + (u / G) * G * 32);
+        return *(const u32x4v*)(fbase + (((2 * (u % G) + h) ^ sw) << 4) + (u / G) * G * 32);
       };
       uint32_t teA = 0, tpA = 0, teB = 0, tpB = 0, epA = 0, epB = 0;
       bool anyA = false, anyB = false;
@@ -647,7 +660,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
           static_for<PIECES + 2 + kE>([&](auto SL) {
             constexpr int s = decltype(SL)::value;
             constexpr int e = s - PIECES - 2;  // epilogue slice index (s >= PIECES + 2)
-            constexpr int at0 = s == 0 ? 0 : s <= PIECES ? 2 * s : s == PIECES + 1 ? 2 * PIECES + 2
+            constexpr int at0 = s == 0 ? 0 : s <= PIECES ? 2 * s : s == PIECES + 1 ? 1
                                 : e < PIECES ? 3 + 2 * e : 2 * PIECES + 3 + (e - PIECES);
             constexpr int at = at0 < 2 * U ? at0 : 2 * U - 1;
             if constexpr (at == st) {
@@ -657,7 +670,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
                   pend = false;
                 }
               } else if constexpr (s <= PIECES) {
-                stage_piece(stile, buf ^ 1, s - 1);
+                stage_piece(stile, sslot, s - 1);
               } else if constexpr (s == PIECES + 1) {
                 nw_p = a.present[w0 + wtile];
                 nw_m = a.mask[w0 + wtile];
@@ -694,11 +707,11 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
         constexpr int kS = PIECES + 1 + 2 * kEpi;
         static_for<kS>([&](auto SL) {
           constexpr int s = decltype(SL)::value;
-          constexpr int at0 = s < PIECES ? 2 + 2 * s : 2 + 2 * PIECES + (s - PIECES);
+          constexpr int at0 = s < PIECES ? 2 + 2 * s : s == PIECES ? 1 : 2 + 2 * PIECES + (s - PIECES);
           constexpr int at = at0 < 2 * U ? at0 : 2 * U - 1;
           if constexpr (at == st) {
             if constexpr (s < PIECES) {
-              if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s);
+              if constexpr (!(ABL & 2)) stage_piece(stile, sslot, s);
             } else if constexpr (s == PIECES) {
               nw_p = a.present[w0 + wtile];
               nw_m = a.mask[w0 + wtile];
@@ -720,8 +733,10 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       pewA = ewA;
       pewB = ewB;
       if constexpr (!(ABL & 4)) {
-        // issued after the last DMA piece: the previous tile's score-image stores
-        constexpr int young = kStores && epi ? 8 : 0;
+        // the youngest vector-memory ops: the DMA pieces of tile + 2 and, after them, the
+        // previous tile's score-image stores — everything older (the next tile's pieces and
+        // words) has landed once at most that many remain (vmcnt retires in order)
+        constexpr int young = (kStores && epi ? 8 : 0) + ((ABL & 2) ? 0 : PIECES);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(young) : "memory");
         __syncthreads();
       }
@@ -736,28 +751,33 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     // one tile with the previous tile's epilogue: sparse when at most kSparseRegs registers can
     // hold an eligible item of it (one uniform branch per tile, decided on the item words)
     constexpr int kSparseRegs = 8;
+    int slot = 0;  // LDS ring slot of the tile being computed
     auto il_step = [&](auto BUF, int tile) __attribute__((always_inline)) {
       if constexpr (LIST) {
         const uint32_t w = __builtin_amdgcn_readfirstlane(ppw & pmw);
         const int pt0 = (tile - 1) * 32;
         const uint32_t u = list_elig16(w, pt0, a.n_valid, 0) | list_elig16(w, pt0, a.n_valid, 1);
         if (__builtin_popcount(u) <= kSparseRegs)
-          il_body(BUF, EY{}, SY{}, tile, u);
+          il_body(BUF, EY{}, SY{}, tile, u, slot);
         else
-          il_body(BUF, EY{}, SN{}, tile, 0u);
+          il_body(BUF, EY{}, SN{}, tile, 0u, slot);
       } else {
-        il_body(BUF, EY{}, SN{}, tile, 0u);
+        il_body(BUF, EY{}, SN{}, tile, 0u, slot);
       }
     };
-    il_body(B0{}, EN{}, SN{}, tile_lo, 0u);
+    auto next_slot = [&]() __attribute__((always_inline)) { slot = slot == 2 ? 0 : slot + 1; };
+    il_body(B0{}, EN{}, SN{}, tile_lo, 0u, slot);
+    next_slot();
     int tile = tile_lo + 1;
     for (;;) {
       if (tile >= tile_hi) break;
       il_step(B1{}, tile);
       ++tile;
+      next_slot();
       if (tile >= tile_hi) break;
       il_step(B0{}, tile);
       ++tile;
+      next_slot();
     }
     // both blocks' epilogues of the last tile (not overlapped)
     auto last = [&](f32x16s& lA, f32x16s& lB) __attribute__((always_inline)) {

@@ -226,6 +226,8 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     }
     return cnt;
   };
+  uint32_t Tg = 1u;
+  if (a.ablate & 4) {  // BB_LS_BITWISE (A/B runs): the round-3 bitwise search, one barrier per bit
   uint32_t* xch = hist;  // [2][4] count slots + [4] hi / [4] lo
   {
     uint32_t hi = 0, lo = 0xFFFFu;
@@ -255,7 +257,6 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     if (lane == 0) atomicMax(&misc[M_PM], pm);
   }
   __syncthreads();
-  uint32_t Tg = 1u;
   const uint32_t hi = max(max(xch[8], xch[9]), max(xch[10], xch[11]));
   const uint32_t lo = min(min(xch[12], xch[13]), min(xch[14], xch[15]));
   if (xch[0] + xch[1] + xch[2] + xch[3] >= (uint32_t)K) {
@@ -271,6 +272,55 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
       if (slot[0] + slot[1] + slot[2] + slot[3] >= (uint32_t)K) P = c;
     }
     Tg = P > delta ? P - delta : 1u;
+  }
+  } else {
+    // Two-level histogram of the 16-bit codes (hist cleared at the start): the bin of the K-th
+    // largest code's high byte, then its low byte among the codes of that bin — two passes of
+    // LDS atomics and two block scans (find_bin), nine barriers in all, against one barrier
+    // per bit of the bitwise search (15-16 at a row's usual code range)
+    uint32_t* scan = (uint32_t*)(dsm + kLsOffScan);
+    auto codes_of = [&](int i, uint32_t (&c)[5]) __attribute__((always_inline)) {
+      c[0] = v[i].x >> 16;
+      c[1] = v[i].x & 0xFFFFu;
+      c[2] = v[i].y >> 16;
+      c[3] = v[i].y & 0xFFFFu;
+      c[4] = v[i].z >> 16;
+    };
+#pragma unroll
+    for (int i = 0; i < kLPT; ++i) {
+      if (i >= nlw) continue;  // wave-uniform
+      uint32_t c[5];
+      codes_of(i, c);
+#pragma unroll
+      for (int e = 0; e < 5; ++e)
+        if (c[e]) atomicAdd(&hist[c[e] >> 8], 1u);
+    }
+    if (want_r0) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) pm = max(pm, (uint32_t)__shfl_xor((int)pm, o));
+      if (lane == 0) atomicMax(&misc[M_PM], pm);
+    }
+    __syncthreads();
+    uint32_t* fb = scan + 4;
+    find_bin(hist, 256, (uint32_t)K, fb, scan);
+    const uint32_t b1 = fb[0], above1 = fb[1];
+    if (b1 != 0xFFFFFFFFu) {  // (uniform) at least K codes
+      hist[tid] = 0u;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < kLPT; ++i) {
+        if (i >= nlw) continue;
+        uint32_t c[5];
+        codes_of(i, c);
+#pragma unroll
+        for (int e = 0; e < 5; ++e)
+          if (c[e] && (c[e] >> 8) == b1) atomicAdd(&hist[c[e] & 0xFFu], 1u);
+      }
+      __syncthreads();
+      find_bin(hist, 256, (uint32_t)K - above1, fb, scan);
+      const uint32_t T0 = (b1 << 8) | fb[0];
+      Tg = T0 > delta ? T0 - delta : 1u;
+    }
   }
   stamp(2);
 
