@@ -117,6 +117,26 @@ def family_kernels(workload, dtype, B, scan_name):
             "finalize": "finalize1_kernel"}
 
 
+def scan_read_roofline(B, d, scan_us, n=N_ITEMS, cus=256):
+    """the f32 index's scan never reads the f32 rows §8(d) prices — it reads
+    their f16 re-rank copy and f16 query operands.  Two more honest denominators for the scan:
+    (1) the bytes it must read (f16 rows + f16 queries) against HBM peak; (2) the per-CU
+    operand-delivery floor: a B × n score block split over P CUs needs at least 2·√(B·n/P)·d·2
+    bytes delivered to each CU (square tiles), at the per-CU rates tools/percu_probe measured
+    (profiles/r05_percu_probe.jsonl, 256 KiB per CU: 66.9 GB/s from a shared, L2-resident
+    region; 25.3 GB/s from regions each XCD must fetch from the Infinity Cache)."""
+    must = n * d * 2 + B * d * 2
+    t = scan_us * 1e-6
+    per_cu = 2.0 * (B * n / cus) ** 0.5 * d * 2
+    rates = {"l2_shared": 66.9e9, "infinity_cache": 25.3e9}
+    floors = {k: per_cu / r * 1e6 for k, r in rates.items()}
+    return {"must_read_bytes": must, "achieved_gbs": round(must / t / 1e9, 1),
+            "frac_hbm_peak": round(must / t / 1e9 / HBM_PEAK_GBS, 4),
+            "operand_bytes_per_cu": round(per_cu), "delivery_floor_us": {k: round(v, 2) for k, v in floors.items()},
+            "frac_of_delivery_floor": {k: round(v / scan_us, 4) for k, v in floors.items()},
+            "source": "profiles/r05_percu_probe.jsonl (tools/percu_probe.hip)"}
+
+
 def dominant_roofline(fam_us, names, flops, alg_bytes, step_us, dtype, scan_mpf, pmc_key):
     """roofline object for the kernel family that takes the most device time per step (HIP
     events, bb_get_profile), with SURVEY.md §8(d)'s algorithmic work of one search priced
@@ -719,6 +739,9 @@ def main():
     step_us = 1e6 * el / args.steps
     roof = dominant_roofline(fam_us, family_kernels(args.workload, args.dtype, B, kname), flops, alg_bytes, step_us,
                              args.dtype, mpf, pmc_key)
+    if args.dtype == "f32" and "gemm" in fam_us:
+        # (hybrid: both sides, the CF factors padded to 64 f16 columns in the re-rank copy)
+        roof["scan_reads"] = scan_read_roofline(B, DIM + (64 if hybrid else 0), fam_us["gemm"])
 
     # ---- MALL-cold latency (256 MiB Infinity Cache flushed before each step) ----
     flush = torch.empty(640 << 20, dtype=torch.uint8, device=dev)

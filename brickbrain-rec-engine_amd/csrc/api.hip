@@ -1376,8 +1376,45 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
             ga_dual0 = ga;  // launched with side 1's
           } else if (dual) {
             if ((rc = timed(x, K_GEMM, s, [&] { return launch_scan4_dual(ga_dual0, ga, s); }))) return rc;
-          } else if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(BF16, ga, s); }))) {
-            return rc;
+          } else {
+            // BB_SCAN_TRACE (probe runs): phase stamps of the list scan's workgroups (scan4)
+            static const bool scan_trace = ab_env("BB_SCAN_TRACE") != nullptr;
+            const bool tr = scan_trace && ga.lists && scan4_used(BF16, bpad);
+            if (tr) {
+              if ((rc = x->trace.ensure((size_t)4096 * 64))) return rc;
+              BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)4096 * 64, s));
+              ga.trace = (uint64_t*)x->trace.p;
+            }
+            if ((rc = timed(x, K_GEMM, s, [&] { return launch_gemm(BF16, ga, s); }))) return rc;
+            if (tr) {
+              std::vector<uint64_t> t((size_t)4096 * 8);
+              BB_HIP(hipMemcpyAsync(t.data(), x->trace.p, t.size() * 8, hipMemcpyDeviceToHost, s));
+              BB_HIP(hipStreamSynchronize(s));
+              uint64_t t0 = ~0ull, t1 = 0;
+              double acc[6] = {0}, tiles = 0, cyc = 0;
+              int nwg = 0, n5 = 0;
+              for (size_t w = 0; w < 4096; ++w) {
+                const uint64_t* r = &t[w * 8];
+                if (!r[0] || !r[5]) continue;
+                ++nwg;
+                t0 = std::min(t0, r[0]);
+                t1 = std::max(t1, r[5]);
+                for (int j = 1; j < 6; ++j)
+                  if (j != 3 || r[3]) acc[j] += (double)(r[j] - r[0]);
+                n5 += r[3] != 0;
+                tiles += (double)r[6];
+                cyc += (double)r[7];
+              }
+              double st = 0;
+              for (size_t w = 0; w < 4096; ++w)
+                if (t[w * 8] && t[w * 8 + 5]) st += (double)(t[w * 8] - t0);
+              nwg = std::max(nwg, 1);
+              fprintf(stderr, "[bb scan trace] side=%d wgs=%d tiles/wg=%.1f us-from-wg-start: prologue %.2f tile1 %.2f "
+                      "tile5 %.2f loop %.2f end %.2f | start skew avg %.2f | span %.2f | shader clock %.2f GHz\n", (int)cf_side, nwg,
+                      tiles / nwg, acc[1] / nwg / 100, acc[2] / nwg / 100, n5 ? acc[3] / n5 / 100 : 0.0,
+                      acc[4] / nwg / 100, acc[5] / nwg / 100, st / nwg / 100, (double)(t1 - t0) / 100,
+                      acc[5] > 0 ? cyc / (acc[5] / 100.0) / 1e3 : 0.0);
+            }
           }
         } else if (cf_side ? s3_f : s3_c) {
           // split-precision scan: items, gathered rows and prepped queries are bf16 planes

@@ -36,6 +36,10 @@
 namespace bb {
 
 constexpr int kScan4Queries = kScanWaves * 64;  // queries per workgroup
+#ifndef BB_SCAN4_PF
+#define BB_SCAN4_PF 4
+#endif
+constexpr int kScan4Pf = BB_SCAN4_PF;  // interleaved schedule: LDS fragment prefetch distance (k-steps)
 
 // Item chunks of a scan4 launch: ~256 workgroups (one per CU).
 inline int scan4_n_chunks(int Mpad, int tiles) {
@@ -176,6 +180,13 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   const int r = lane & 31, h = lane >> 5;
   const int qA = group * kScan4Queries + wave * 64 + r, qB = qA + 32;
   if (tile_lo >= tile_hi) return;  // uniform per workgroup
+  // BB_SCAN_TRACE probe runs (a.trace): s_memrealtime stamps, 8 words per workgroup — start,
+  // query prologue done, first tile, fifth tile, loop done, end; word 6 = tiles
+  auto stamp = [&](int slot) __attribute__((always_inline)) {
+    if (a.trace && tid == 0) a.trace[(size_t)L * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  const uint64_t clk0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;  // shader clock (word 7: cycles)
+  stamp(0);
 
   // LDS fragment addresses (scan2 layout: chunk (2u + h) ^ swz(r) of row r) and LDS-DMA
   // source offsets are recomputed per use (a few VALU in the MFMA shadow) instead of held
@@ -350,6 +361,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  stamp(1);
   // consume every plain load now (no LDS-DMA outstanding): the compiler's own waits for
   // them would otherwise land behind later staging and wait for it
   asm volatile("" : "+v"(pw), "+v"(mw), "+v"(ewA), "+v"(ewB));
@@ -582,6 +594,9 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     // and both blocks' epilogues of tile t-1 are woven into tile t, after its DMA pieces.
     f32x16s accA1 = {}, accB1 = {};
     uint32_t pewA = 0;
+    int fxo[G];  // LDS byte offset of chunk (2g + h) ^ swz of this lane's row (scan2 layout)
+#pragma unroll
+    for (int g = 0; g < G; ++g) fxo[g] = ((2 * g + h) ^ swz) << 4;
     // Sparse list epilogue (masks: configs[2]'s ~2 % dense constraint mask).  The mask and the
     // item space are per item, so whether accumulator register g can hold an eligible item is
     // the same for every lane of a half: u = the union over both halves (uniform).  When u has
@@ -619,24 +634,25 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       const int stile = tile + 2 < tile_hi ? tile + 2 : tile;
       const int sslot = slot == 0 ? 2 : slot - 1;
       const int wtile = tile + 1 < tile_hi ? tile + 1 : tile;
+      // fragment addresses from the per-lane chunk offsets fxo (registers are not short on this
+      // schedule): one add per distinct chunk and tile, the k-group offset an immediate
       const char* fbase = smem + slot * TILE_B + rrow;
       auto frag = [&](int u) __attribute__((always_inline)) {
-        int sw = swz;
-        asm volatile("" : "+v"(sw));
-        return *(const u32x4v*)(fbase + (((2 * (u % G) + h) ^ sw) << 4) + (u / G) * G * 32);
+        return *(const u32x4v*)(fbase + fxo[u % G] + (u / G) * G * 32);
       };
       uint32_t teA = 0, tpA = 0, teB = 0, tpB = 0, epA = 0, epB = 0;
       bool anyA = false, anyB = false;
-      u32x4v fq[4];
-      fq[0] = frag(0);
-      if constexpr (U > 1) fq[1] = frag(1);
+      // fragment ring in k-steps: prefetch distance PF (BB build knob kScan4Pf), ring PF + 2
+      constexpr int PF = KU <= 48 ? kScan4Pf : 2, NR = PF + 2;  // (d = 512: no registers for more)
+      u32x4v fq[NR];
+      static_for<(PF < U ? PF : U)>([&](auto II) { fq[decltype(II)::value] = frag(decltype(II)::value); });
       static_for<2 * U>([&](auto SS) {
         constexpr int st = decltype(SS)::value;
         constexpr int u = st >> 1, b = st & 1;
-        // fragment ring in k-steps (prefetch distance 2); fragment u-1 stays live until A_u
-        // has issued (inline-asm MFMAs are opaque to hazard tracking)
-        if constexpr (b == 0 && u + 2 < U) fq[(u + 2) % 4] = frag(u + 2);
-        const u32x4v fv = fq[u % 4];
+        // fragment u-1 stays live until A_u has issued (inline-asm MFMAs are opaque to hazard
+        // tracking)
+        if constexpr (b == 0 && u + PF < U) fq[(u + PF) % NR] = frag(u + PF);
+        const u32x4v fv = fq[u % NR];
         f32x16s& c = b ? cB : cA;
         if constexpr (u == 0) {
           if constexpr (F16)
@@ -649,7 +665,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
           else
             asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "a"(qv[b * U + u]));
         }
-        if constexpr (b == 0 && u > 0) asm volatile("" ::"v"(fq[(u + 3) % 4]));
+        if constexpr (b == 0 && u > 0) asm volatile("" ::"v"(fq[(u + NR - 1) % NR]));
         if constexpr (st == 1 && epi) asm volatile("s_nop 15" : "+v"(pA), "+v"(pB));
         if constexpr (LIST) {
           // slices: the pending period store (step 0, ahead of the DMA), DMA pieces (even
@@ -767,6 +783,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     };
     auto next_slot = [&]() __attribute__((always_inline)) { slot = slot == 2 ? 0 : slot + 1; };
     il_body(B0{}, EN{}, SN{}, tile_lo, 0u, slot);
+    stamp(2);
     next_slot();
     int tile = tile_lo + 1;
     for (;;) {
@@ -778,7 +795,9 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       il_step(B0{}, tile);
       ++tile;
       next_slot();
+      if (tile == tile_lo + 5) stamp(3);
     }
+    stamp(4);
     // both blocks' epilogues of the last tile (not overlapped)
     auto last = [&](f32x16s& lA, f32x16s& lB) __attribute__((always_inline)) {
       asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" : "+v"(lA), "+v"(lB));
@@ -795,6 +814,9 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
           if (liveB) *(uint2*)(a.r0lists + 2 * list_slot(chunk, 0, 1, l_nb, qB >> 5, lane)) = make_uint2(r0B.k0, r0B.k1);
         }
         list_put(l_period, lstA.pack(), lstB.pack());  // the last (possibly partial) period
+        if (a.trace && tid == 0) a.trace[(size_t)L * 8 + 6] = (uint64_t)(tile_hi - tile_lo);
+        if (a.trace && tid == 0) a.trace[(size_t)L * 8 + 7] = __builtin_amdgcn_s_memtime() - clk0;
+        stamp(5);
         return;
       }
       uint32_t te = 0, tp = 0, ep = 0;

@@ -29,13 +29,15 @@ def child():
     _, _, run, _, _ = bench.make_lane(brickrec, "c3", base, 1024, 0, dev, 0, 0, 1, extra)
     print("searching", flush=True)
     for _ in range(4):
-        run()
+        run.prof_run()   # bb_search itself (a plan records its launches once; the traces sync per search)
     torch.cuda.synchronize()
 
 
 def main():
     os.environ["BB_AB"] = "1"  # (read by the library at its first search)
-    if "--no-trace" not in sys.argv:
+    if "--scan" in sys.argv:
+        os.environ["BB_SCAN_TRACE"] = "1"      # the list scans' phase stamps (scan4)
+    elif "--no-trace" not in sys.argv:
         os.environ["BB_SELECT_TRACE"] = "1"
     child()
     print("c3 trace run ok", flush=True)

@@ -11,8 +11,8 @@
 #include <cstdio>
 #include <vector>
 
-__global__ __launch_bounds__(256) void k_vec(const uint4* __restrict__ src, size_t per_wg, uint32_t* out) {
-  const uint4* p = src + (size_t)blockIdx.x * (per_wg / 16);
+__global__ __launch_bounds__(256) void k_vec(const uint4* __restrict__ src, size_t per_wg, uint32_t* out, int share) {
+  const uint4* p = src + (size_t)(blockIdx.x / share) * (per_wg / 16);
   const int n = (int)(per_wg / 16);
   uint32_t acc = 0;
   int i = threadIdx.x;
@@ -24,9 +24,9 @@ __global__ __launch_bounds__(256) void k_vec(const uint4* __restrict__ src, size
   if (acc == 0x12345678u) out[0] = acc;
 }
 
-__global__ __launch_bounds__(256) void k_lds(const char* __restrict__ src, size_t per_wg, uint32_t* out) {
+__global__ __launch_bounds__(256) void k_lds(const char* __restrict__ src, size_t per_wg, uint32_t* out, int share) {
   __shared__ __attribute__((aligned(16))) char ring[2][4096 * 4];
-  const char* p = src + (size_t)blockIdx.x * per_wg;
+  const char* p = src + (size_t)(blockIdx.x / share) * per_wg;
   const uint32_t base = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)&ring[0][0]);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int pieces = (int)(per_wg / 16384);  // 16 KiB per step: each wave 4 KiB = four 1-KiB pieces
@@ -56,12 +56,16 @@ int main() {
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  for (size_t per : {65536ul, 131072ul, 262144ul, 524288ul, 1048576ul}) {
+  // share = consecutive workgroups reading the same region (8: an XCD's eight CUs under the
+  // round-robin placement do NOT share; consecutive blockIdx land on different XCDs, so share 8
+  // spreads each region over all XCDs' L2s — the MALL serves it once per XCD)
+  for (int share : {1, 8, 64})
+  for (size_t per : {65536ul, 262144ul, 1048576ul}) {
     for (int variant = 0; variant < 2; ++variant) {
       // kernel-accurate times: the launch carries the events (the dispatch's own begin / end)
       auto runx = [&](hipEvent_t e0, hipEvent_t e1) {
-        if (variant == 0) hipExtLaunchKernelGGL(k_vec, dim3(wgs), dim3(256), 0, 0, e0, e1, 0, (const uint4*)buf, per, out);
-        else hipExtLaunchKernelGGL(k_lds, dim3(wgs), dim3(256), 0, 0, e0, e1, 0, (const char*)buf, per, out);
+        if (variant == 0) hipExtLaunchKernelGGL(k_vec, dim3(wgs), dim3(256), 0, 0, e0, e1, 0, (const uint4*)buf, per, out, share);
+        else hipExtLaunchKernelGGL(k_lds, dim3(wgs), dim3(256), 0, 0, e0, e1, 0, (const char*)buf, per, out, share);
       };
       auto run = [&] { runx(nullptr, nullptr); };
       for (int i = 0; i < 3; ++i) run();
@@ -76,8 +80,8 @@ int main() {
       }
       std::sort(t.begin(), t.end());
       const float us = t[t.size() / 2];
-      printf("{\"variant\":\"%s\",\"bytes_per_cu\":%zu,\"us_p50\":%.2f,\"bytes_per_cu_per_us\":%.0f,"
-             "\"chip_gbs\":%.0f}\n", variant ? "lds_dma" : "vector_loads", per, us, per / us,
+      printf("{\"variant\":\"%s\",\"share\":%d,\"bytes_per_cu\":%zu,\"us_p50\":%.2f,\"bytes_per_cu_per_us\":%.0f,"
+             "\"chip_gbs\":%.0f}\n", variant ? "lds_dma" : "vector_loads", share, per, us, per / us,
              per * wgs / us / 1e3);
     }
   }
