@@ -446,6 +446,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
                         ListTop5& L, ListTop2& R, uint32_t& e16, bool& full, uint32_t& kodd) __attribute__((always_inline)) {
     constexpr int s = decltype(SS)::value;
     const int ptile0 = ptile * 32;
+    if constexpr (ABL & 1) return;  // (probe: no epilogue)
     if constexpr (s == 0) {
       e16 = list_elig16(epw & emw & ~eew, ptile0, a.n_valid, h);
       full = __all(e16 == 0xFFFFu);
@@ -603,19 +604,25 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     // at most kSparseRegs registers, the list epilogue of the previous tile inserts only those
     // (a scalar loop, the register picked by a uniform index) instead of all sixteen register
     // pairs — the masked-out ones would insert code 0, a no-op.  The lists are the same keys.
-    auto list_sparse = [&](const f32x16s& p, int ptile, uint32_t eew, float k2, ListTop5& L, ListTop2& R,
-                           uint32_t u) __attribute__((always_inline)) {
+    // in three slices per block, each woven into its own MFMA gap: 0 the lane's eligibility
+    // word, 1 the inserts of the registers u names, 2 rank 0 (the present maximum)
+    auto list_sparse = [&](auto SS, const f32x16s& p, int ptile, uint32_t eew, float k2, ListTop5& L, ListTop2& R,
+                           uint32_t u, uint32_t& e16) __attribute__((always_inline)) {
+      constexpr int s = decltype(SS)::value;
+      if constexpr (ABL & 1) return;  // (probe: no epilogue)
       const int ptile0 = ptile * 32;
-      const uint32_t e16 = list_elig16(ppw & pmw & ~eew, ptile0, a.n_valid, h);
-      const uint32_t pb = (uint32_t)l_cnt << 4;
-      for (uint32_t uu = u; uu; uu &= uu - 1u) {
-        const int g = __builtin_ctz(uu);
-        const float v = p[g];
-        const uint32_t c =
-            __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_u16(fmaf(v, k2, 0.5f), 0.f)) & 0xFFFFu;
-        L.ins(((e16 >> g) & 1u) ? (c << 16) | pb | (uint32_t)g : 0u);
-      }
-      if (a.r0lists) {
+      if constexpr (s == 0) {
+        e16 = list_elig16(ppw & pmw & ~eew, ptile0, a.n_valid, h);
+      } else if constexpr (s == 1) {
+        const uint32_t pb = (uint32_t)l_cnt << 4;
+        for (uint32_t uu = u; uu; uu &= uu - 1u) {
+          const int g = __builtin_ctz(uu);
+          const float v = p[g];
+          const uint32_t c =
+              __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_u16(fmaf(v, k2, 0.5f), 0.f)) & 0xFFFFu;
+          L.ins(((e16 >> g) & 1u) ? (c << 16) | pb | (uint32_t)g : 0u);
+        }
+      } else if (a.r0lists) {
         const float m = list_present_max(p, list_elig16(ppw, ptile0, a.n_valid, h));
         R.ins(list_r0_key(m, k2, (uint32_t)(ptile - tile_lo)));
       }
@@ -672,7 +679,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
           // steps from 2), the next tile's words, then the previous tile's list epilogue of
           // block A and block B (odd steps between the pieces, then one per step) and the
           // period counter
-          constexpr int kE = SP ? 3 : 2 * kLE + 1;
+          constexpr int kE = SP ? 7 : 2 * kLE + 1;
           static_for<PIECES + 2 + kE>([&](auto SL) {
             constexpr int s = decltype(SL)::value;
             constexpr int e = s - PIECES - 2;  // epilogue slice index (s >= PIECES + 2)
@@ -693,9 +700,11 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
                 nw_eA = erowA[w0 + wtile];
                 nw_eB = erowB[w0 + wtile];
               } else if constexpr (epi) {
-                if constexpr (SP && e < 2) {
-                  if constexpr (e == 0) list_sparse(pA, tile - 1, pewA, k2A, lstA, r0A, su);
-                  else list_sparse(pB, tile - 1, pewB, k2B, lstB, r0B, su);
+                if constexpr (SP && e < 6) {
+                  if constexpr (e < 3)
+                    list_sparse(std::integral_constant<int, e>{}, pA, tile - 1, pewA, k2A, lstA, r0A, su, le16A);
+                  else
+                    list_sparse(std::integral_constant<int, e - 3>{}, pB, tile - 1, pewB, k2B, lstB, r0B, su, le16B);
                 } else if constexpr (!SP && e < kLE) {
                   list_slice(std::integral_constant<int, e>{}, pA, tile - 1, ppw, pmw, pewA, k2A, lstA, r0A, le16A, lfullA,
                              lkoA);
