@@ -491,16 +491,25 @@ __device__ __forceinline__ uint32_t sq_gather(const SqArgs& a, const uint64_t* t
   const float margin = sq_margin_row(a, qv);
   uint32_t top;
   if (kth) {  // the largest multiple of 2^16 with >= K list keys at or above it (every key of
-              // every list is a distinct item, so K of them reach it: counting the workgroup
-              // maxima alone left the bound at 0 when fewer than K workgroups hold an item)
+              // every list is a distinct item, so K of them reach it).  The workgroup maxima
+              // alone are counted while at least 2K workgroups hold an eligible item (a quarter of
+              // the ballots on the merge's latency chain); below that, every key (the maxima
+              // alone left the bound at 0 when fewer than K workgroups hold one: ADVICE r04)
+    int nz = 0;  // workgroups holding an eligible item (a selective mask can leave few)
+#pragma unroll
+    for (int i = 0; i < NL; ++i) nz += __popcll(__ballot(ent[i][0] != 0ull));
+    const bool all_keys = nwg < 2 * K || nz < 2 * K;  // (uniform)
     uint32_t prefix = 0;
     for (int bit = 31; bit >= 16; --bit) {
       const uint32_t c = prefix | (1u << bit);
       int cnt = 0;
 #pragma unroll
-      for (int i = 0; i < NL; ++i)
+      for (int i = 0; i < NL; ++i) {
+        cnt += __popcll(__ballot(ordk_of(ent[i][0]) >= c));
+        if (all_keys)
 #pragma unroll
-        for (int j = 0; j < kSqM; ++j) cnt += __popcll(__ballot(ordk_of(ent[i][j]) >= c));
+          for (int j = 1; j < kSqM; ++j) cnt += __popcll(__ballot(ordk_of(ent[i][j]) >= c));
+      }
       if (cnt >= K) prefix = c;
     }
     top = prefix;
