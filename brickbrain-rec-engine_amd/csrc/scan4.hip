@@ -74,6 +74,7 @@ hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t
 int scan4_pilot_m(int kpad) { return kpad * 2 / 16 <= 64 ? 8 : 4; }
 
 bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s) {
+  if (a.ldx <= 0 || a.ldx >= (int64_t(1) << 23)) return false;  // 24-bit DMA offsets (scan4_kernel.h)
   if (ku <= kRrMaxD / 8) {  // the exact re-rank path first (the f16 copy of an f32 index)
     bool launched = false;
     if ((launch_scan4_rr_lo(a, ku, s, launched) || launch_scan4_rr_hi(a, ku, s, launched)) && launched) return true;

@@ -195,31 +195,44 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   const int rrow = r * ROWB;
   const char* Xg = (const char*)a.X;
   const size_t ldxb = (size_t)a.ldx * sizeof(T);
+  // LDS-DMA source offset of this lane's 16 B in piece p, relative to the tile's first row
+  // (launch_scan4 guarantees ldx < 2^23, so it fits 32 bits and every product is 24-bit):
+  // chunk c of the tile image -> row c / KU by multiply-shift (exact for c < 32·KU), chunk
+  // (c mod KU) ^ swz(row).  ~7 full-rate VALU; the tile base rides in SGPRs (saddr form), so
+  // no 64-bit address math per piece (the signed 64-bit form cost ~28 issue slots a piece,
+  // ~20 % of the d = 768 scan)
+  static_assert(32 * KU * KU < (1 << 20), "row = c * kDivM >> 20 exact for c < 32 KU");
+  constexpr uint32_t kDivM = ((1u << 20) + KU - 1) / KU;
+  const uint32_t ldxb32 = (uint32_t)ldxb;
   auto soff = [&](int p) __attribute__((always_inline)) {
-    int ln = lane;
+    uint32_t ln = lane;
     asm volatile("" : "+v"(ln));  // opaque per use: no hoisted per-piece registers
-    const int mine = (wave * PIECES + p) * 1024 + ln * 16;
-    const int row = mine / ROWB;
-    const int ch = ((mine % ROWB) >> 4) ^ scan_swz<KU>(row);
-    return (size_t)row * ldxb + ch * 16;
+    const uint32_t c = (uint32_t)(wave * PIECES + p) * 64u + ln;
+    const uint32_t row = __umul24(c, kDivM) >> 20;
+    uint32_t cin;  // c - row·KU as one full-rate 24-bit mad (the compiler picks a 64-bit one)
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(cin) : "v"(row), "s"(-KU), "v"(c));
+    const uint32_t ch = cin ^ (uint32_t)scan_swz<KU>((int)row);
+    return __umul24(row, ldxb32) + (ch << 4);
   };
   const uint32_t lds_base = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
   // interleaved schedule (d <= 512): the query operand leaves registers for the per-piece
-  // source offsets — precomputed once (each recomputation is ~20 VALU of integer division,
-  // ~130 per tile at d = 384, on a VALU-bound list epilogue)
+  // source offsets — precomputed once (the list epilogue there is VALU-bound)
   uint32_t soffr[IL ? PIECES : 1];
   if constexpr (IL) {
 #pragma unroll
-    for (int p = 0; p < PIECES; ++p) soffr[p] = (uint32_t)soff(p);
+    for (int p = 0; p < PIECES; ++p) soffr[p] = soff(p);
   }
   // inline asm, as in scan2: the compiler's waitcnt pass must not wait for these
   auto stage_piece = [&](int tile, int buf, int p) __attribute__((always_inline)) {
-    size_t so;
+    uint32_t so;
     if constexpr (IL) so = soffr[p];
     else so = soff(p);
-    const char* src = Xg + (size_t)tile * 32 * ldxb + so;
+    const uint64_t tb = (uint64_t)(size_t)(Xg + (size_t)tile * 32 * ldxb);
+    const char* src = (const char*)(size_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32)) << 32) |
+                                            __builtin_amdgcn_readfirstlane((uint32_t)tb));
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + buf * TILE_B + (wave * PIECES + p) * 1024);
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory");
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(dst), "v"(so), "s"(src)
+                 : "memory");
   };
 
   // first tile(s) in flight before the query loads
