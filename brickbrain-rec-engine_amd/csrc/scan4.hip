@@ -57,7 +57,8 @@ hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t
       !scan4_used(BF16, a0.Mpad) ||
       !a0.lists != !a1.lists || (a0.lists && (a0.l_period <= 0 || a0.l_np <= 0 || a1.l_period <= 0 || a1.l_np <= 0)) ||
       a0.Mpad != a1.Mpad || a0.Ncols % 32 || a1.Ncols % 32 || (a0.slab_start & 31) || (a1.slab_start & 31) || a0.q_ids ||
-      a0.q_src || a0.q_istats || a1.q_ids || a1.q_src || a1.q_istats)
+      a0.q_src || a0.q_istats || a1.q_ids || a1.q_src || a1.q_istats || a0.ldx <= 0 || a0.ldx >= (int64_t(1) << 23) ||
+      a1.ldx <= 0 || a1.ldx >= (int64_t(1) << 23))  // 24-bit DMA offsets (scan4_kernel.h)
     return hipErrorInvalidValue;
   bool ok = false;
   switch (ku0) {

@@ -228,8 +228,10 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     if constexpr (IL) so = soffr[p];
     else so = soff(p);
     const uint64_t tb = (uint64_t)(size_t)(Xg + (size_t)tile * 32 * ldxb);
-    const char* src = (const char*)(size_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32)) << 32) |
-                                            __builtin_amdgcn_readfirstlane((uint32_t)tb));
+    // (readfirstlane returns int: widen through uint32_t, or the low word sign-extends)
+    const uint32_t tlo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tb);
+    const uint32_t thi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32));
+    const char* src = (const char*)(size_t)(((uint64_t)thi << 32) | (uint64_t)tlo);
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + buf * TILE_B + (wave * PIECES + p) * 1024);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(dst), "v"(so), "s"(src)
                  : "memory");
