@@ -40,6 +40,10 @@ constexpr int kScan4Queries = kScanWaves * 64;  // queries per workgroup
 #define BB_SCAN4_PF 4
 #endif
 constexpr int kScan4Pf = BB_SCAN4_PF;  // interleaved schedule: LDS fragment prefetch distance (k-steps)
+#ifndef BB_SCAN4_CHAIN_PF
+#define BB_SCAN4_CHAIN_PF 2
+#endif
+constexpr int kScan4ChainPf = BB_SCAN4_CHAIN_PF;  // chained (d = 768) schedule: the same, in MFMA steps
 
 // Item chunks of a scan4 launch: ~256 workgroups (one per CU).
 inline int scan4_n_chunks(int Mpad, int tiles) {
@@ -164,9 +168,13 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   constexpr bool F16 = (ABL & kScanF16) != 0;  // f16 operands: the re-rank copy of an f32 index
   // item tile ring — three tiles deep on the interleaved schedule (two tiles of LDS-DMA in flight
   // while one is read: the ring the MALL / L2 latency needs at one workgroup per CU), two on the
-  // chained d = 768 one (no LDS left) — + (streaming) a 4-KiB register parking area per wave
-  constexpr int RING = IL ? 3 : 2;
-  __shared__ __attribute__((aligned(16))) char smem[RING * TILE_B + (STREAM ? kScanWaves * 4096 : 0)];
+  // chained d = 768 one — + (streaming) a 4-KiB register parking area per wave.  ABL 128
+  // (probe): three on the chained one too (three 48-KiB tiles + the park = all 160 KiB) —
+  // measured equal (tools/scan4_probe: the chained loop is bound by LDS bandwidth, not latency)
+  constexpr int kParkB = STREAM ? kScanWaves * 4096 : 0;
+  constexpr int RING = (IL || (ABL & 128)) ? 3 : 2;
+  static_assert(RING * TILE_B + kParkB <= 163840, "LDS ring + park exceed 160 KiB");
+  __shared__ __attribute__((aligned(16))) char smem[RING * TILE_B + kParkB];
 
   const int n_groups = a.Mpad / kScan4Queries;
   const int total = n_groups * n_chunks;
@@ -497,29 +505,33 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
 
   // One tile: chain A over buffer BUF (+ block B's epilogue of tile-1 when EPIB), chain B
   // (+ block A's epilogue of this tile).
-  auto tile_body = [&](auto BUF, auto EPIB, int tile) __attribute__((always_inline)) {
-    constexpr int buf = decltype(BUF)::value;
+  // The LDS ring slot of the tile is a runtime value (one tile body, not one per slot): the
+  // slot's row base goes in one register per tile, the chunk offset is recomputed per use.
+  // Staging runs RING - 1 tiles ahead, into the slot tile - 1 read (free since its barrier).
+  auto tile_body = [&](auto EPIB, int tile, int slot) __attribute__((always_inline)) {
     constexpr bool epib = decltype(EPIB)::value;
-    const int stile = tile + 1 < tile_hi ? tile + 1 : tile;  // branch-free staging target
-    const int wtile = stile;                                 // words of the next tile
+    const int stile = tile + RING - 1 < tile_hi ? tile + RING - 1 : tile;  // branch-free staging target
+    const int sslot = RING == 3 ? (slot == 0 ? 2 : slot - 1) : slot ^ 1;
+    const int wtile = tile + 1 < tile_hi ? tile + 1 : tile;  // words of the next tile
+    const char* fb = smem + slot * TILE_B + rrow;
     auto frag = [&](int u) __attribute__((always_inline)) {
       int sw = swz;
       asm volatile("" : "+v"(sw));  // opaque per use: no hoisted per-u address registers
-      return *(const u32x4v*)(smem + buf * TILE_B + rrow + (((2 * (u % G) + h) ^ sw) << 4) + (u / G) * G * 32);
+      return *(const u32x4v*)(fb + (((2 * (u % G) + h) ^ sw) << 4) + (u / G) * G * 32);
     };
     uint32_t teB = 0, tpB = 0, teA = 0, tpA = 0, epA = 0, epB = 0;
     bool anyA = false, anyB = false;
-    // 4-slot fragment ring over both chains (step s: block s / U, k-step s % U), prefetch
-    // distance 2; a fragment stays live one step past its MFMA (inline-asm MFMAs are opaque
-    // to hazard tracking: no ds_read may land in registers an in-flight MFMA still reads)
-    u32x4v fq[4];
-    fq[0] = frag(0);
-    fq[1] = frag(1 % U);
+    // (PFC + 2)-slot fragment ring over both chains (step s: block s / U, k-step s % U),
+    // prefetch distance PFC; a fragment stays live one step past its MFMA (inline-asm MFMAs
+    // are opaque to hazard tracking: no ds_read may land in registers an in-flight MFMA reads)
+    constexpr int PFC = kScan4ChainPf, NRC = PFC + 2;
+    u32x4v fq[NRC];
+    static_for<PFC>([&](auto II) { fq[decltype(II)::value] = frag(decltype(II)::value % U); });
     static_for<2 * U>([&](auto SS) {
       constexpr int st = decltype(SS)::value;
       constexpr int b = st / U, u = st % U;
-      if constexpr (st + 2 < 2 * U) fq[(st + 2) % 4] = frag((st + 2) % U);
-      const u32x4v fv = fq[st % 4];
+      if constexpr (st + PFC < 2 * U) fq[(st + PFC) % NRC] = frag((st + PFC) % U);
+      const u32x4v fv = fq[st % NRC];
       f32x16s& c = b ? accB : accA;
       if constexpr (st < NA) {
         if constexpr (u == 0) {
@@ -548,7 +560,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
             asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "v"(qv[st]));
         }
       }
-      if constexpr (st > 0) asm volatile("" ::"v"(fq[(st + 3) % 4]));
+      if constexpr (st > 0) asm volatile("" ::"v"(fq[(st + NRC - 1) % NRC]));
       // the other block's accumulator: its chain ended >= 2 MFMAs ago; the tie makes every
       // VALU read of it come after this point, with an extra wait for the MFMA to retire
       if constexpr (u == 1) {
@@ -570,7 +582,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
               nw_eA = erowA[w0 + wtile];
               nw_eB = erowB[w0 + wtile];
             } else {
-              if constexpr (!(ABL & 2)) stage_piece(stile, buf ^ 1, s - kEpi - 1);
+              if constexpr (!(ABL & 2)) stage_piece(stile, sslot, s - kEpi - 1);
             }
           }
         });
@@ -585,8 +597,11 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     pmw = mw;
     pewB = ewB;
     if constexpr (!(ABL & 4)) {
-      // issued after the last DMA piece: block A's score-image stores (chain B)
-      constexpr int young = kStores ? 4 : 0;
+      // the youngest vector-memory ops: block A's score-image stores (chain B), issued after
+      // the last DMA piece, and (three-deep ring) the pieces of tile + 2 — everything older
+      // (the next tile's pieces, the words) has landed once at most that many remain (vmcnt
+      // retires in order; streaming appends after the pieces only make the wait longer)
+      constexpr int young = (kStores ? 4 : 0) + (RING == 3 && !(ABL & 2) ? PIECES : 0);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(young) : "memory");
       __syncthreads();
     }
@@ -864,15 +879,12 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       }
     }
   } else {
-  tile_body(B0{}, EN{}, tile_lo);
+  int slot = 0;  // LDS ring slot of the tile being computed
+  tile_body(EN{}, tile_lo, slot);
   int tile = tile_lo + 1;
-  for (;;) {
-    if (tile >= tile_hi) break;
-    tile_body(B1{}, EY{}, tile);
-    ++tile;
-    if (tile >= tile_hi) break;
-    tile_body(B0{}, EY{}, tile);
-    ++tile;
+  for (; tile < tile_hi; ++tile) {
+    slot = slot == RING - 1 ? 0 : slot + 1;
+    tile_body(EY{}, tile, slot);
   }
   // block B's epilogue of the last tile (not overlapped)
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" : "+v"(accB));

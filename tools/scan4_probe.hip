@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "../brickbrain-rec-engine_amd/csrc/scan4_kernel.h"
@@ -44,9 +45,11 @@ void l2(const GemmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((scan2_kernel<uint16_t, KU, ABL>), dim3(a.Mpad / 128 * nc), dim3(256), 0, s, a, nc, tiles);
 }
 
-int main() {
+int main(int argc, char** argv) {
   const int M = 4096;
+  const char* only = argc > 1 ? argv[1] : "012";  // configs to run (e.g. "02")
   for (int cfg = 0; cfg < 3; ++cfg) {
+    if (!strchr(only, '0' + cfg)) continue;
     const int D = cfg == 1 ? 384 : 768;
     const int N = cfg == 2 ? 1048576 : 131072;  // cfg 2: items far beyond the MALL (1.6 GB)
     uint16_t *q, *x;
@@ -101,9 +104,13 @@ int main() {
       vs = {{"s4_no_stores", l4<96, 24>, 0}, {"s4_no_stores_c32", l4<96, 24>, 32},
             {"s4_stream_nohit", l4s<96, 0>, 0}, {"s4_stream_real", l4s<96, 1>, 0},
             {"s4_stream_real_noflush", l4s<96, 1, 32>, 0}, {"s4_stream_real_nostore", l4s<96, 1, 64>, 0},
-            {"s4_no_staging", l4<96, 2 | 24>, 0}};  // (scan2 ABL 8|16 still stores the last tile: S is sized for 131072 columns)
+            {"s4_no_staging", l4<96, 2 | 24>, 0},
+            // ABL 128: a three-deep LDS ring on the chained schedule (A/B)
+            {"s4_no_stores_ring3", l4<96, 24 | 128>, 0}, {"s4_stream_nohit_ring3", l4s<96, 0, 128>, 0},
+            {"s4_stream_real_ring3", l4s<96, 1, 128>, 0}};  // (scan2 ABL 8|16 still stores the last tile: S is sized for 131072 columns)
     else if (D == 768)
-      vs = {{"s4_full", l4<96, 0>, 0}, {"s4_no_stores", l4<96, 24>, 0}, {"s4_no_epi", l4<96, 1>, 0},
+      vs = {{"s4_full", l4<96, 0>, 0}, {"s4_full_ring3", l4<96, 128>, 0}, {"s4_no_stores_ring3", l4<96, 24 | 128>, 0},
+            {"s4_no_stores", l4<96, 24>, 0}, {"s4_no_epi", l4<96, 1>, 0},
             {"s4_no_stores_nobarrier", l4<96, 24 | 4>, 0}, {"s4_no_stores_nostage_nobarrier", l4<96, 24 | 4 | 2>, 0},
             {"s4_no_staging", l4<96, 2 | 24>, 0}, {"s4_mfma_lds_only", l4<96, 7>, 0},
             {"s4_no_stores_c32", l4<96, 24>, 32}, {"s4_no_stores_c64", l4<96, 24>, 64},
