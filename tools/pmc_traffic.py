@@ -21,7 +21,7 @@ FAMILIES = {
     "gemm": ("bb::scan3_kernel", "bb::scan2_kernel", "bb::scan4_kernel", "bb::scan4_dual_kernel",
              "bb::(anonymous namespace)::sq_scan_kernel"),
     "select": ("bb::select_list_kernel", "bb::select_list_dual_kernel", "bb::select_kernel", "bb::select_rr_wave",
-               "bb::cand_select_kernel", "bb::pilot_bound", "bb::(anonymous namespace)::sq_merge_kernel"),
+               "bb::cand_select_kernel", "bb::cand_select_wave_kernel", "bb::pilot_bound", "bb::(anonymous namespace)::sq_merge_kernel"),
     "prep": ("bb::prep_kernel", "bb::prep2_kernel"),
     "finalize": ("bb::finalize1_kernel", "bb::finalize_kernel"),
     "rerank": ("bb::rerank_kernel",),
