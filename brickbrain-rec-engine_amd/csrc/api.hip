@@ -12,6 +12,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -146,7 +147,7 @@ struct bb_index {
   DevBuf qh, qcfh;                   // re-rank: per-query quanta of the int16 score image
   DevBuf rr_out, rr_cnt, rr_thr, rr_r0, rr_r0n;  // re-rank: select -> rerank hand-off
   // streaming top-K (large indexes): pilot lists, candidate regions, overflow flag
-  DevBuf pilot, cand, cand_cnt, cand_pmax, ovf;
+  DevBuf pilot, cand, cand_cnt, cand_pmax;
   DevBuf pilot_top;  // kScanPilot scans: per lane the top-m half-tile maxima of the pilot rows
   DevBuf trace;        // BB_SELECT_TRACE probe stamps
   DevBuf rr_flags;     // one-wave re-rank select: rows left to the block select
@@ -228,11 +229,23 @@ int s_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStre
   BB_HIP(hipMemcpyAsync(dst, src, bytes, kind, s));
   return BB_OK;
 }
+// Host wait for the work queued on s.  BB_SPIN_WAIT (A/B): 1 polls hipStreamQuery, 2 polls
+// and yields between polls, instead of hipStreamSynchronize's blocking wait.
+hipError_t host_wait(hipStream_t s) {
+  static const int mode = ab_env("BB_SPIN_WAIT") ? atoi(ab_env("BB_SPIN_WAIT")) : 0;
+  if (!mode) return hipStreamSynchronize(s);
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) return e;
+    if (mode == 2) std::this_thread::yield();
+  }
+}
+
 int s_sync(hipStream_t s) {
   if (tl_capture)
     return fail(BB_E_STATE, "bb_plan_create: this search synchronises with the host (the streaming top-K of a large "
                             "index): use bb_search");
-  BB_HIP(hipStreamSynchronize(s));
+  BB_HIP(host_wait(s));
   return BB_OK;
 }
 
@@ -462,7 +475,7 @@ int bb_destroy(bb_index* x) {
     }
     for (DevBuf* b : {&x->items, &x->items_present, &x->ones, &x->zeros, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S, &x->tmax,
                       &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
-                      &x->cand, &x->cand_cnt, &x->cand_pmax, &x->ovf, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
+                      &x->cand, &x->cand_cnt, &x->cand_pmax, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
                       &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
                       &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists, &x->pilot_top,
                       &x->sq_top, &x->sq_ptop, &x->sq_ords})
@@ -1101,11 +1114,14 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     if (refine && ((rc = x->list1.ensure((size_t)Bc * K_int * 8)) || (rc = x->max1.ensure((size_t)Bc * 8))))
       return rc;
     if ((rc = x->pilot.ensure((size_t)Bc * K_int * 8)) || (rc = x->cand.ensure(need_keys * 8)) ||
-        (rc = x->cand_cnt.ensure(need_rg * 4)) || (rc = x->cand_pmax.ensure(need_rg * 8)) ||
-        (rc = x->ovf.ensure(256)))
+        (rc = x->cand_cnt.ensure(need_rg * 4)) || (rc = x->cand_pmax.ensure(need_rg * 8)))
       return rc;
-    if (!x->ovf_host) BB_HIP(hipHostMalloc((void**)&x->ovf_host, 4, hipHostMallocDefault));
-    if ((rc = s_memset(x->ovf.p, 0, 4, s))) return rc;
+    // the overflow flag: coherent pinned host memory the candidate selects store into, cleared
+    // here by the host (every earlier search on this index has completed: the stream path
+    // waits for its flag before returning) and read after the search's one wait — no fill or
+    // copy launch on the path
+    if (!x->ovf_host) BB_HIP(hipHostMalloc((void**)&x->ovf_host, 64, hipHostMallocCoherent));
+    *(volatile uint32_t*)x->ovf_host = 0u;
   }
 
   for (int64_t b0 = 0; b0 < B; b0 += Bc) {
@@ -1458,7 +1474,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           ca.regions = regions;
           ca.cap = cand_cap;
           ca.K = K_int;
-          ca.overflow = (uint32_t*)x->ovf.p;
+          ca.overflow = x->ovf_host;
           if (!last_spass) {  // pass A of the two-level bound: the exact list of [0, n1)
             ca.keys_out = (uint64_t*)x->list1.p;
             ca.max_out = side_drop ? (uint64_t*)x->max1.p : nullptr;
@@ -1752,10 +1768,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   if (stream) {
     // a candidate region overflowed (masses of equal scores, a pilot sample unlike the rest):
     // the caller reruns the search on the exact slab path
-    if ((rc = s_sync(s))) return rc;  // (fails a plan before the host copy is recorded)
-    BB_HIP(hipMemcpyAsync(x->ovf_host, x->ovf.p, 4, hipMemcpyDeviceToHost, s));
-    BB_HIP(hipStreamSynchronize(s));
-    if (*x->ovf_host && ab_env("BB_STREAM_DEBUG")) {
+    if (tl_capture) return s_sync(s);  // (fails the plan: the host reads the flag)
+    BB_HIP(host_wait(s));
+    const uint32_t overflowed = *(volatile uint32_t*)x->ovf_host;
+    if (overflowed && ab_env("BB_STREAM_DEBUG")) {
       int rg, cap;
       const int bpl = (int)pad_rows(B - (B - 1) / Bc * Bc);
       stream_geom(bpl, refine ? 1 : 0, rg, cap);
@@ -1778,7 +1794,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
               (long long)n0, K_int, bpl, rg, cap, mx, arg, arg / rg, sum / cnt.size(), over, zero_rows,
               (unsigned long long)pk[K_int - 1]);
     }
-    if (*x->ovf_host) return kRetrySlab;
+    if (overflowed) return kRetrySlab;
   }
   if (host_out) {
     BB_HIP(hipMemcpyAsync(res->scores, o_sc, (size_t)B * q->k * 4, hipMemcpyDeviceToHost, s));
@@ -1863,7 +1879,7 @@ int bb_finalize(bb_index* x, const bb_query* q, const uint64_t* keys, const uint
     BB_HIP(hipMemcpyAsync(res->scores, x->out_sc.p, (size_t)B * q->k * 4, hipMemcpyDeviceToHost, s));
     BB_HIP(hipMemcpyAsync(res->ids, x->out_id.p, (size_t)B * q->k * 8, hipMemcpyDeviceToHost, s));
     if (res->counts) BB_HIP(hipMemcpyAsync(res->counts, x->out_cnt.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
-    BB_HIP(hipStreamSynchronize(s));
+    BB_HIP(host_wait(s));
   }
   return scope.leave();
 }

@@ -25,6 +25,13 @@
 
 namespace bb {
 
+// The streaming path's overflow flag lives in pinned host memory (the host reads it after its
+// one wait, no copy back): every writer stores 1 — a system-scope store, not a read-modify-
+// write, so it needs no PCIe atomics.
+__device__ __forceinline__ void flag_set(uint32_t* f) {
+  __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 constexpr int kCandCap = 2048;                  // candidate capacity
 constexpr int kOffHist = kMaxKInt * 8;          // radix path: cand[0..kMaxKInt) then hist
 constexpr int kRegionA = kOffHist + 4096 * 4;   // 20 KiB, reused by both paths
@@ -642,7 +649,7 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
       gm = k > gm ? k : gm;
     }
   }
-  if (__any(ovf) && lane == 0) atomicOr(a.overflow, 1u);
+  if (__any(ovf) && lane == 0) flag_set(a.overflow);
   uint32_t total;
   uint32_t off = block_excl_scan(sum, scan_sh, total);
 #pragma unroll
@@ -939,7 +946,7 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_wave_kernel(CandSe
       gm = k > gm ? k : gm;
     }
   }
-  if (__any(ovf) && lane == 0) atomicOr(a.overflow, 1u);
+  if (__any(ovf) && lane == 0) flag_set(a.overflow);
   uint32_t incl = sum;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
