@@ -688,25 +688,33 @@ def main():
     torch.cuda.synchronize()
 
     # ---- timed region: K steps, barrier + sync on both sides, max over ranks ----
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # (nothing but the steps inside: a pair of per-step events costs the host about as much
+    # as a plan launch, and at 20 steps the host would pace the pipeline fill)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    for i in range(args.steps):
+        lanes[i % len(lanes)][2]()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+
+    # ---- per-step latency with batches in flight (p50_ms): the same K steps again, untimed,
+    # each bracketed by events on its lane's stream ----
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     for i in range(args.steps):
         _, s_i, run_i, _, _ = lanes[i % len(lanes)]
         ev[i][0].record(s_i)
         run_i()
         ev[i][1].record(s_i)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
     lat_ms = np.array([a.elapsed_time(b) for a, b in ev])
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
 
     # ---- per-kernel device time (HIP events on the launch stream), same K steps, one batch
     # at a time (lane 0 alone: kernel averages not inflated by the other lanes' batches) ----
