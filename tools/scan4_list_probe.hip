@@ -26,14 +26,17 @@ __global__ void fill_f16(uint16_t* p, size_t n, uint32_t seed) {
   }
 }
 
-template <int ABL>
+template <int KU, int ABL>
 void launch(const GemmArgs& a, int nc, int tiles, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  hipExtLaunchKernelGGL((scan4_kernel<48, kScanList | kScanF16 | ABL>), dim3(a.Mpad / 256 * nc), dim3(256), 0, s, e0,
+  hipExtLaunchKernelGGL((scan4_kernel<KU, kScanList | kScanF16 | ABL>), dim3(a.Mpad / 256 * nc), dim3(256), 0, s, e0,
                         e1, 0, a, nc, tiles);
 }
 
-int main() {
-  const int M = 1024, N = 25216, D = 384, tiles = (N + 127) / 128 * 4;
+// the configs[2] content side (d = 384, KU 48) or, with argument "cf", its CF side (r = 50
+// padded to 64, KU 8)
+template <int KU>
+int run(const char* side) {
+  const int M = 1024, N = 25216, D = KU * 8, tiles = (N + 127) / 128 * 4;
   uint16_t *q, *x;
   uint32_t *lists, *ones, *zeros, *mask2;
   float* sh;
@@ -59,7 +62,7 @@ int main() {
     std::vector<float> h(M, 1e-4f);
     (void)hipMemcpy(sh, h.data(), M * 4, hipMemcpyHostToDevice);
   }
-  const int nc = scan4_list_chunks(M, tiles, 48);
+  const int nc = scan4_list_chunks(M, tiles, KU);
   const int tpc = (tiles + nc - 1) / nc;
   GemmArgs a{};
   a.Q = q; a.X = x; a.ldq = a.ldx = D; a.Mpad = M; a.Ncols = tiles * 32; a.Kpad = D;
@@ -71,9 +74,10 @@ int main() {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   struct V { const char* name; void (*f)(const GemmArgs&, int, int, hipStream_t, hipEvent_t, hipEvent_t); };
-  std::vector<V> vs = {{"full", launch<0>}, {"no_epilogue", launch<1>}, {"no_staging", launch<2>},
-                       {"no_wait_barrier", launch<4>}, {"mfma_lds_only", launch<7>}, {"no_query_loads", launch<2048>},
-                       {"no_epi_no_query_loads", launch<2048 | 1>}, {"mfma_lds_no_query_loads", launch<2048 | 7>}};
+  std::vector<V> vs = {{"full", launch<KU, 0>}, {"no_epilogue", launch<KU, 1>}, {"no_staging", launch<KU, 2>},
+                       {"no_wait_barrier", launch<KU, 4>}, {"mfma_lds_only", launch<KU, 7>},
+                       {"no_query_loads", launch<KU, 2048>}, {"no_epi_no_query_loads", launch<KU, 2048 | 1>},
+                       {"mfma_lds_no_query_loads", launch<KU, 2048 | 7>}};
   for (int m = 0; m < 2; ++m) {
     a.mask = m ? mask2 : ones;
     for (auto& v : vs) {
@@ -87,10 +91,15 @@ int main() {
       }
       if (hipStreamSynchronize(s) != hipSuccess) { printf("{\"error\":\"%s\"}\n", v.name); return 1; }
       std::sort(t.begin(), t.end());
-      printf("{\"mask\":\"%s\",\"variant\":\"%s\",\"us_p50\":%.2f,\"tflops\":%.0f,\"chunks\":%d}\n", m ? "1.7%" : "all",
-             v.name, t[6], 2.0 * M * N * D / (t[6] * 1e-6) / 1e12, nc);
+      printf("{\"side\":\"%s\",\"mask\":\"%s\",\"variant\":\"%s\",\"us_p50\":%.2f,\"tflops\":%.0f,\"chunks\":%d}\n", side,
+             m ? "1.7%" : "all", v.name, t[6], 2.0 * M * N * D / (t[6] * 1e-6) / 1e12, nc);
       fflush(stdout);
     }
   }
   return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'c') return run<8>("cf");
+  return run<48>("content");
 }

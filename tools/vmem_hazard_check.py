@@ -115,7 +115,14 @@ def check_function(name, insns):
                     break
                 if mn2 == "s_branch" or mn2.startswith("s_cbranch"):
                     t = TARGET.search(ops2)
-                    k = index.get(base + int(t.group(2), 16)) if t else None
+                    if t:
+                        k = index.get(base + int(t.group(2), 16))
+                    else:  # no label printed: the SOPP immediate, in dwords from the next instruction
+                        mi = re.match(r"\s*(-?\d+)", ops2)
+                        simm = int(mi.group(1)) if mi else None
+                        if simm is not None and simm >= 1 << 15:
+                            simm -= 1 << 16
+                        k = index.get(a2 + 4 + 4 * simm) if simm is not None else None
                     if k is None:
                         bad.append(f"{name}: unresolved branch at {a2 - base:#x}")
                         break
