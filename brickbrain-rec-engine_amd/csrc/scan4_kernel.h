@@ -174,7 +174,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   constexpr int kParkB = STREAM ? kScanWaves * 4096 : 0;
   constexpr int RING = (IL || (ABL & 128)) ? 3 : 2;
   static_assert(RING * TILE_B + kParkB <= 163840, "LDS ring + park exceed 160 KiB");
-  __shared__ __attribute__((aligned(16))) char smem[RING * TILE_B + kParkB];
+  __shared__ __attribute__((aligned(256))) char smem[RING * TILE_B + kParkB];
 
   const int n_groups = a.Mpad / kScan4Queries;
   const int total = n_groups * n_chunks;
@@ -514,10 +514,25 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     const int sslot = RING == 3 ? (slot == 0 ? 2 : slot - 1) : slot ^ 1;
     const int wtile = tile + 1 < tile_hi ? tile + 1 : tile;  // words of the next tile
     const char* fb = smem + slot * TILE_B + rrow;
+    // Fragment u: chunk (2g + h) ^ swz of this lane's row, g = u % G, k-group u / G.  With rows
+    // and slots whole multiples of 256 B (the LDS array starts 256-aligned), fb's low 8 bits are
+    // zero and (2g + h) ^ swz = 2g ^ (h ^ swz), so fb + 16·((2g + h) ^ swz) = fbc ^ 32g with
+    // fbc = fb | 16·(h ^ swz): ONE v_xor per read (an asm statement, so it is recomputed per
+    // use instead of hoisted into G registers the d = 768 schedule does not have), the k-group
+    // an immediate.  The old form took three VALU per read in the MFMA gaps.
+    constexpr bool kXorFrag = ROWB % 256 == 0 && TILE_B % 256 == 0;
+    const uint32_t fbc = (uint32_t)(size_t)((const __attribute__((address_space(3))) char*)fb) | (uint32_t)((h ^ swz) << 4);
     auto frag = [&](int u) __attribute__((always_inline)) {
-      int sw = swz;
-      asm volatile("" : "+v"(sw));  // opaque per use: no hoisted per-u address registers
-      return *(const u32x4v*)(fb + (((2 * (u % G) + h) ^ sw) << 4) + (u / G) * G * 32);
+      if constexpr (kXorFrag) {
+        uint32_t ad = fbc;
+        if (u % G) asm volatile("v_xor_b32 %0, %1, %2" : "=v"(ad) : "i"((u % G) * 32), "v"(fbc));
+        return *(const __attribute__((address_space(3))) u32x4v*)((const __attribute__((address_space(3))) char*)(size_t)ad +
+                                                                 (u / G) * G * 32);
+      } else {
+        int sw = swz;
+        asm volatile("" : "+v"(sw));  // opaque per use: no hoisted per-u address registers
+        return *(const u32x4v*)(fb + (((2 * (u % G) + h) ^ sw) << 4) + (u / G) * G * 32);
+      }
     };
     uint32_t teB = 0, tpB = 0, teA = 0, tpA = 0, epA = 0, epB = 0;
     bool anyA = false, anyB = false;
