@@ -164,6 +164,36 @@ def test_cf_rated_excluded(brickrec):
         idx.close()
 
 
+@pytest.mark.parametrize("scale", [1e-35, 1e-30])
+def test_tiny_query_rows(brickrec, scale):
+    """Query rows far below f16 range: the pass scales a row by 2^(14 - e) of its
+    largest |q|, the exponent clamped at 126 — 1e-35 rows would otherwise scale to +inf and
+    NaN orders.  Raw CF rows (no normalisation) and semantic rows (normalised by the path)."""
+    n, r, B = 6000, 50, 5
+    rng = np.random.default_rng(31)
+    x = R.unit_rows(n, 64, 8)
+    f = rng.normal(0, 0.1, (n, r)).astype(np.float32)
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x, prenormalized=True)
+        idx.upload_cf(f)
+        u = (rng.normal(0, 1.0, (B, r)) * scale).astype(np.float32)
+        sc, ids, cnt = _all_variants(idx, "cf", 10, q_cf=u)
+        for b in range(B):
+            ri, rs = _exact(f, u[b], 10, np.ones(n, bool))
+            assert list(ids[b]) == list(ri)
+            assert np.array_equal(sc[b].view(np.uint32), rs.view(np.uint32))
+        q = (R.unit_rows(B, 64, 9) * scale).astype(np.float32)
+        sc, ids, cnt = _all_variants(idx, "semantic", 10, q_rows=q)
+        rows = idx.get_rows(np.arange(n))
+        qn = _qop(q)
+        for b in range(B):
+            ri, rs = _exact(rows, qn[b], 10, np.ones(n, bool))
+            assert list(ids[b]) == list(ri)
+    finally:
+        idx.close()
+
+
 def test_f16_range_saturation(brickrec):
     """Values beyond the f16 range (|x| > 65504) saturate in the approximate copy and in the
     query operands; every bound is computed from the saturated values, so those rows and
