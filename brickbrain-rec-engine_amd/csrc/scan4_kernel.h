@@ -672,15 +672,6 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
         R.ins(list_r0_key(m, k2, (uint32_t)(ptile - tile_lo)));
       }
     };
-    // the next tile's eligibility words, by asm: issued before the tile's DMA pieces and retired
-    // by the end-of-tile wait that names them (below); tests/test_asm_hazard.py checks on the
-    // shipped code that nothing touches the registers in between
-    auto load_words = [&](int wt) __attribute__((always_inline)) {
-      asm volatile("global_load_dword %0, %1, off" : "=v"(nw_p) : "v"(a.present + w0 + wt) : "memory");
-      asm volatile("global_load_dword %0, %1, off" : "=v"(nw_m) : "v"(a.mask + w0 + wt) : "memory");
-      asm volatile("global_load_dword %0, %1, off" : "=v"(nw_eA) : "v"(erowA + w0 + wt) : "memory");
-      asm volatile("global_load_dword %0, %1, off" : "=v"(nw_eB) : "v"(erowB + w0 + wt) : "memory");
-    };
     auto il_body = [&](auto BUF, auto EPI, auto SPC, int tile, uint32_t su, int slot) __attribute__((always_inline)) {
       constexpr int buf = decltype(BUF)::value;  // accumulator set (tile parity); LDS ring slot: `slot`
       constexpr bool epi = decltype(EPI)::value;
@@ -749,7 +740,10 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
               } else if constexpr (s <= PIECES) {
                 stage_piece(stile, sslot, s - 1);
               } else if constexpr (s == PIECES + 1) {
-                load_words(wtile);
+                nw_p = a.present[w0 + wtile];
+                nw_m = a.mask[w0 + wtile];
+                nw_eA = erowA[w0 + wtile];
+                nw_eB = erowB[w0 + wtile];
               } else if constexpr (epi) {
                 if constexpr (SP && e < 6) {
                   if constexpr (e < 3)
@@ -789,7 +783,10 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
             if constexpr (s < PIECES) {
               if constexpr (!(ABL & 2)) stage_piece(stile, sslot, s);
             } else if constexpr (s == PIECES) {
-              load_words(wtile);
+              nw_p = a.present[w0 + wtile];
+              nw_m = a.mask[w0 + wtile];
+              nw_eA = erowA[w0 + wtile];
+              nw_eB = erowB[w0 + wtile];
             } else if constexpr (epi) {
               constexpr int e = s - PIECES - 1;
               if constexpr (e < kEpi)
@@ -805,18 +802,13 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       pmw = mw;
       pewA = ewA;
       pewB = ewB;
-      // the youngest vector-memory ops: the DMA pieces of tile + 2 and, after them, the
-      // previous tile's score-image stores — everything older (the next tile's pieces and
-      // words) has landed once at most that many remain (vmcnt retires in order).  The words
-      // were loaded by asm: the wait names them "+v" in the same statement (scan2's rule), so
-      // the compiler places no wait of its own for them — a plain C++ load got a vmcnt(0)
-      // after the barrier, which also waited for tile + 2's DMA and left one tile of prefetch
       if constexpr (!(ABL & 4)) {
+        // the youngest vector-memory ops: the DMA pieces of tile + 2 and, after them, the
+        // previous tile's score-image stores — everything older (the next tile's pieces and
+        // words) has landed once at most that many remain (vmcnt retires in order)
         constexpr int young = (kStores && epi ? 8 : 0) + ((ABL & 2) ? 0 : PIECES);
-        asm volatile("s_waitcnt vmcnt(%4)" : "+v"(nw_p), "+v"(nw_m), "+v"(nw_eA), "+v"(nw_eB) : "n"(young) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(young) : "memory");
         __syncthreads();
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(nw_p), "+v"(nw_m), "+v"(nw_eA), "+v"(nw_eB) : : "memory");  // (probe)
       }
       pw = nw_p;
       mw = nw_m;

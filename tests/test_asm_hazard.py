@@ -1,5 +1,5 @@
-"""The inline-asm eligibility loads of scan2_kernel.h and scan4_kernel.h's
-interleaved schedule (round 5): on the SHIPPED
+"""The inline-asm eligibility loads of scan2_kernel.h, and every scan4
+kernel: on the SHIPPED
 library, no instruction names a `global_load_dword` destination register between the load and
 a `s_waitcnt vmcnt` that retires it, on any control-flow path (tools/vmem_hazard_check.py).
 CPU only: the code object is extracted and disassembled with the ROCm LLVM tools."""
@@ -56,8 +56,9 @@ def test_shipped_scan2_loads_are_retired_before_use():
 
 @needs_tools
 def test_shipped_scan4_loads_are_retired_before_use():
-    """scan4's interleaved schedule loads its words by asm too (round 5): the same CFG walk
-    over every scan4 instantiation (the dual kernel's bodies included)."""
+    """The same CFG walk over every scan4 instantiation (the dual kernel's bodies included):
+    its asm LDS-DMA sits between plain loads and their compiler-placed waits, and an asm word
+    load (tried in round 5, reverted: configs[4] 2 % slower) would be checked here too."""
     kernels, sites, bad = H.run(pattern=r"scan4_(dual_)?kernel")
     assert kernels >= 20, kernels
     assert sites >= 200, sites
