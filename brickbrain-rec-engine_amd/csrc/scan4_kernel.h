@@ -562,17 +562,19 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
         }
       } else {
         // VGPR-resident query operand: the s_nop covers a VALU write (a copy the register
-        // allocator may place) -> MFMA read hazard the compiler cannot see through asm
+        // allocator may place) -> MFMA read hazard the compiler cannot see through asm — two
+        // wait states (cdna_hip_programming.md §5.7: a just-written "v" operand -> MFMA
+        // operand, s_nop 1; it was s_nop 4, three cycles more in 32 of every 96 MFMA gaps)
         if constexpr (u == 0) {
           if constexpr (F16)
-            asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "v"(qv[st]));
+            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "v"(qv[st]));
           else
-            asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "v"(qv[st]));
+            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(fv), "v"(qv[st]));
         } else {
           if constexpr (F16)
-            asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "v"(qv[st]));
+            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "v"(qv[st]));
           else
-            asm volatile("s_nop 4\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "v"(qv[st]));
+            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fv), "v"(qv[st]));
         }
       }
       if constexpr (st > 0) asm volatile("" ::"v"(fq[(st + NRC - 1) % NRC]));
