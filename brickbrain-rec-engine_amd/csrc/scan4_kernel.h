@@ -225,15 +225,18 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   const uint32_t lds_base = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
   // interleaved schedule (d <= 512): the query operand leaves registers for the per-piece
   // source offsets — precomputed once (the list epilogue there is VALU-bound)
-  uint32_t soffr[IL ? PIECES : 1];
-  if constexpr (IL) {
+  // (the chained d = 768 schedule too, since its stream epilogue stopped holding sixteen mask
+  // constants in VGPRs: 7 VALU less per piece in the MFMA gaps, 12 pieces a tile)
+  constexpr bool kSoffR = true;
+  uint32_t soffr[kSoffR ? PIECES : 1];
+  if constexpr (kSoffR) {
 #pragma unroll
     for (int p = 0; p < PIECES; ++p) soffr[p] = soff(p);
   }
   // inline asm, as in scan2: the compiler's waitcnt pass must not wait for these
   auto stage_piece = [&](int tile, int buf, int p) __attribute__((always_inline)) {
     uint32_t so;
-    if constexpr (IL) so = soffr[p];
+    if constexpr (kSoffR) so = soffr[p];
     else so = soff(p);
     const uint64_t tb = (uint64_t)(size_t)(Xg + (size_t)tile * 32 * ldxb);
     // (readfirstlane returns int: widen through uint32_t, or the low word sign-extends)
@@ -425,13 +428,14 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     } else if constexpr (STREAM) {
       if constexpr (s <= 4) {
         if (any) {
+          // four bits from inline constants (1, 2, 4, 8), shifted once: selects of 1 << (16 + g)
+          // made the compiler hold sixteen constants in VGPRs for the whole loop
+          constexpr int g0 = 4 * (s - 1);
           uint32_t m = 0;
 #pragma unroll
-          for (int gg = 0; gg < 4; ++gg) {
-            constexpr int g0 = 4 * (s - 1);
-            m |= p[g0 + gg] >= sl.thrf ? 1u << (16 + g0 + gg) : 0u;
-          }
-          ep |= m;
+          for (int gg = 0; gg < 4; ++gg) m |= p[g0 + gg] >= sl.thrf ? 1u << gg : 0u;
+          asm volatile("" : "+v"(m));  // (keeps the shift out of the select constants)
+          ep |= m << (16 + g0);
         }
       } else if constexpr (s == 5) {
         if constexpr (!(ABL & 32))
