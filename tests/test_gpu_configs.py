@@ -192,9 +192,10 @@ def _sharded_vs_unsharded(brickrec, x, q, k, P, n_check, chunk, name):
         n_diff += int((dif != 0).sum())
     assert n_diff <= 8, (name, n_diff)
     print(f"[parity] {name}: {n} stored bf16 rows vs torch conversion, {n_diff} elements differ by 1 ulp")
-    # f64 recompute for n_check queries spread over the batch
+    # f64 recompute for n_check queries spread over the batch (every query: round 5), on the
+    # device in 64K-row chunks (B x 65,536 f64 scores at a time)
     rows_q = torch.linspace(0, B - 1, n_check, device=dev).long()
-    rs, ri = _f64_topk(full, _bf16_query_operand(q[rows_q]), n, k, chunk)
+    rs, ri = _f64_topk(full, _bf16_query_operand(q[rows_q]), n, k, 1 << 16)
     sc_h, ids_h = sc[rows_q].cpu().numpy(), ids[rows_q].cpu().numpy()
     gate = Gate(name)
     for j in range(n_check):
@@ -230,7 +231,7 @@ def test_c3_1M_768_bf16_b4096_sharded(brickrec):
     dev = torch.device("cuda", 0)
     x = _unit_rows_dev(1_000_000, 768, 1234, dev)
     q = _unit_rows_dev(4096, 768, 4321, dev)
-    _sharded_vs_unsharded(brickrec, x, q, 100, 8, 512, 1 << 18, "configs[3] 1M x 768 bf16 B=4096 top-100")
+    _sharded_vs_unsharded(brickrec, x, q, 100, 8, 4096, 1 << 18, "configs[3] 1M x 768 bf16 B=4096 top-100")
 
 
 def test_c4_10M_384_bf16_b8192_sharded(brickrec):
@@ -238,7 +239,7 @@ def test_c4_10M_384_bf16_b8192_sharded(brickrec):
     dev = torch.device("cuda", 0)
     x = _unit_rows_dev(10_000_000, 384, 1234, dev)
     q = _unit_rows_dev(8192, 384, 4321, dev)
-    _sharded_vs_unsharded(brickrec, x, q, 100, 8, 256, 1 << 20, "configs[4] 10M x 384 bf16 B=8192 top-100")
+    _sharded_vs_unsharded(brickrec, x, q, 100, 8, 8192, 1 << 20, "configs[4] 10M x 384 bf16 B=8192 top-100")
 
 
 # --------------------------------------------------------------------------- sharded hybrid
