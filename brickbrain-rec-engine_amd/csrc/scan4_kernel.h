@@ -417,7 +417,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       tile_maxima(p, ptile0, a.n_valid, epw, ok, h, te, tp);
       if constexpr (STREAM) {
         any = __any(te >= sl.thr);
-        ep = s4_elig16(ok, ptile0, a.n_valid, h);
+        if (any) ep = s4_elig16(ok, ptile0, a.n_valid, h);  // (read only by the compare / append slices)
       }
       if constexpr (PILOT) {
         if (q == qA) pm_ins(pmA, te);

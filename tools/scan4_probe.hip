@@ -47,11 +47,12 @@ void l2(const GemmArgs& a, hipStream_t s) {
 
 int main(int argc, char** argv) {
   const int M = 4096;
-  const char* only = argc > 1 ? argv[1] : "012";  // configs to run (e.g. "02")
-  for (int cfg = 0; cfg < 3; ++cfg) {
+  const char* only = argc > 1 ? argv[1] : "0123";  // configs to run (e.g. "02")
+  for (int cfg = 0; cfg < 4; ++cfg) {
     if (!strchr(only, '0' + cfg)) continue;
-    const int D = cfg == 1 ? 384 : 768;
-    const int N = cfg == 2 ? 1048576 : 131072;  // cfg 2: items far beyond the MALL (1.6 GB)
+    const int D = cfg == 1 || cfg == 3 ? 384 : 768;
+    // cfg 2: items far beyond the MALL (1.6 GB); cfg 3: the d = 384 streaming scan (configs[4]'s)
+    const int N = cfg >= 2 ? 1048576 : 131072;
     uint16_t *q, *x;
     float* S;
     uint32_t *tm, *pm, *ones, *zeros;
@@ -90,7 +91,7 @@ int main(int argc, char** argv) {
     {
       std::vector<uint64_t> h(M, 0xFFFFFFFF00000000ull);
       (void)hipMemcpy(thr_none, h.data(), M * 8, hipMemcpyHostToDevice);
-      const uint32_t o = ord_of(0.066f);
+      const uint32_t o = ord_of(D == 384 ? 0.047f : 0.066f);  // ~0.2 % of the random scores reach it
       std::fill(h.begin(), h.end(), (uint64_t)o << 32);
       (void)hipMemcpy(thr_real, h.data(), M * 8, hipMemcpyHostToDevice);
     }
@@ -100,7 +101,11 @@ int main(int argc, char** argv) {
     a.cand_cap = cap;
     g_thr_none = thr_none;
     g_thr_real = thr_real;
-    if (cfg == 2)
+    if (cfg == 3)
+      vs = {{"s4_no_stores", l4<48, 24>, 0}, {"s4_stream_nohit", l4s<48, 0>, 0}, {"s4_stream_real", l4s<48, 1>, 0},
+            {"s4_stream_real_noflush", l4s<48, 1, 32>, 0}, {"s4_no_staging", l4<48, 2 | 24>, 0},
+            {"s4_mfma_lds_only", l4<48, 7>, 0}};
+    else if (cfg == 2)
       vs = {{"s4_no_stores", l4<96, 24>, 0}, {"s4_no_stores_c32", l4<96, 24>, 32},
             {"s4_stream_nohit", l4s<96, 0>, 0}, {"s4_stream_real", l4s<96, 1>, 0},
             {"s4_stream_real_noflush", l4s<96, 1, 32>, 0}, {"s4_stream_real_nostore", l4s<96, 1, 64>, 0},
