@@ -148,7 +148,10 @@ constexpr int scan4_atA(int s, int U, int E, int pieces) {
 
 // ABL (tools/scan4_probe only): 1 = no epilogue, 2 = no staging after the first tile, 4 = no
 // per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no streaming
-// appends (compares only), 64 = streaming appends without their stores, 2048 = no query
+// appends (compares only), 64 = streaming appends without their stores, 128 = a three-deep
+// ring on the chained schedule, 256 = the streaming compare slices without their uniform
+// branch (measured: 4 % slower without hits, 2-5 % faster at a 0.2 % hit rate; the real
+// passes are mostly without hits), 1024 = the chained schedule at d <= 512, 2048 = no query
 // loads (zero operand).
 template <int KU, int ABL = 0, bool PM = false>
 __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int tiles_total, int L) {
@@ -427,7 +430,8 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       // (no score image, no maxima rows: the lane's top-PM list is the pilot's output)
     } else if constexpr (STREAM) {
       if constexpr (s <= 4) {
-        if (any) {
+        // (ABL 256, probe: the compares without the uniform branch)
+        if ((ABL & 256) || any) {
           // four bits from inline constants (1, 2, 4, 8), shifted once: selects of 1 << (16 + g)
           // made the compiler hold sixteen constants in VGPRs for the whole loop
           constexpr int g0 = 4 * (s - 1);
