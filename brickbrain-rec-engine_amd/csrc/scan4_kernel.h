@@ -149,10 +149,10 @@ constexpr int scan4_atA(int s, int U, int E, int pieces) {
 // ABL (tools/scan4_probe only): 1 = no epilogue, 2 = no staging after the first tile, 4 = no
 // per-tile wait + barrier, 8 = no S stores, 16 = no tile-maxima stores, 32 = no streaming
 // appends (compares only), 64 = streaming appends without their stores, 128 = a three-deep
-// ring on the chained schedule, 256 = the streaming compare slices without their uniform
-// branch (measured: 4 % slower without hits, 2-5 % faster at a 0.2 % hit rate; the real
-// passes are mostly without hits), 1024 = the chained schedule at d <= 512, 2048 = no query
-// loads (zero operand).
+// ring on the chained schedule, 256 = (with 65536) the streaming compare slices without
+// their uniform branch (measured: 4 % slower without hits, 2-5 % faster at a 0.2 % hit rate), 1024 = the chained schedule at d <= 512, 2048 = no query
+// loads (zero operand), 65536 = the streaming compares and appends woven over slices 1-5 (the
+// round-4 placement) instead of under slice 0's one branch.
 template <int KU, int ABL = 0, bool PM = false>
 __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int tiles_total, int L) {
   typedef uint16_t T;
@@ -420,7 +420,25 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
       tile_maxima(p, ptile0, a.n_valid, epw, ok, h, te, tp);
       if constexpr (STREAM) {
         any = __any(te >= sl.thr);
-        if (any) ep = s4_elig16(ok, ptile0, a.n_valid, h);  // (read only by the compare / append slices)
+        if constexpr (ABL & 65536) {
+          if (any) ep = s4_elig16(ok, ptile0, a.n_valid, h);  // (read by the woven compare / append slices)
+        } else if (any) {
+          // the eligibility, the compares and the appends under ONE uniform branch: a tile
+          // without hits (most of them) pays one branch per block instead of five (~22 cycles
+          // each, 12 % of the d = 384 streaming scan, tools/scan4_probe cfg 3); the hit
+          // bits from inline constants, four at a time (selects of 1 << (16 + g) made the
+          // compiler hold sixteen constants in VGPRs for the whole loop)
+          ep = s4_elig16(ok, ptile0, a.n_valid, h);
+#pragma unroll
+          for (int g0 = 0; g0 < 16; g0 += 4) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) m |= p[g0 + gg] >= sl.thrf ? 1u << gg : 0u;
+            asm volatile("" : "+v"(m));  // (keeps the shift out of the select constants)
+            ep |= m << (16 + g0);
+          }
+          if constexpr (!(ABL & 32)) s4_flush<ABL>(a, p, ptile0, h, (ep >> 16) & ep, sl, region(q), park);
+        }
       }
       if constexpr (PILOT) {
         if (q == qA) pm_ins(pmA, te);
@@ -429,7 +447,10 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     } else if constexpr (PILOT) {
       // (no score image, no maxima rows: the lane's top-PM list is the pilot's output)
     } else if constexpr (STREAM) {
+      // ABL 65536 (probe): the round-4 weave — compares in slices 1-4, appends in slice 5,
+      // each under its own branch; by default they run in slice 0 (above)
       if constexpr (s <= 4) {
+        if constexpr (!(ABL & 65536)) return;
         // (ABL 256, probe: the compares without the uniform branch)
         if ((ABL & 256) || any) {
           // four bits from inline constants (1, 2, 4, 8), shifted once: selects of 1 << (16 + g)
@@ -442,7 +463,7 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
           ep |= m << (16 + g0);
         }
       } else if constexpr (s == 5) {
-        if constexpr (!(ABL & 32))
+        if constexpr ((ABL & 65536) && !(ABL & 32))
           if (any) s4_flush<ABL>(a, p, ptile0, h, (ep >> 16) & ep, sl, region(q), park);
       } else if constexpr (s == 6) {
         if (a.cand_pmax) s4_rank0(a, p, ptile0, epw, h, tp, sl);

@@ -106,7 +106,9 @@ int main(int argc, char** argv) {
             {"s4_stream_real_noflush", l4s<48, 1, 32>, 0}, {"s4_no_staging", l4<48, 2 | 24>, 0},
             {"s4_mfma_lds_only", l4<48, 7>, 0},
             // ABL 256: the compare slices without their uniform branch
-            {"s4_stream_nohit_bf", l4s<48, 0, 256>, 0}, {"s4_stream_real_bf", l4s<48, 1, 256>, 0}};
+            // ABL 65536: the round-4 weave (compares in slices 1-4, appends in slice 5, one branch each)
+            {"s4_stream_nohit_weave", l4s<48, 0, 65536>, 0}, {"s4_stream_real_weave", l4s<48, 1, 65536>, 0},
+            {"s4_stream_nohit_noepi", l4s<48, 0, 1>, 0}};
     else if (cfg == 2)
       vs = {{"s4_no_stores", l4<96, 24>, 0}, {"s4_no_stores_c32", l4<96, 24>, 32},
             {"s4_stream_nohit", l4s<96, 0>, 0}, {"s4_stream_real", l4s<96, 1>, 0},
@@ -115,7 +117,7 @@ int main(int argc, char** argv) {
             // ABL 128: a three-deep LDS ring on the chained schedule (A/B)
             {"s4_no_stores_ring3", l4<96, 24 | 128>, 0}, {"s4_stream_nohit_ring3", l4s<96, 0, 128>, 0},
             {"s4_stream_real_ring3", l4s<96, 1, 128>, 0},
-            {"s4_stream_nohit_bf", l4s<96, 0, 256>, 0}, {"s4_stream_real_bf", l4s<96, 1, 256>, 0}};  // (scan2 ABL 8|16 still stores the last tile: S is sized for 131072 columns)
+            {"s4_stream_nohit_weave", l4s<96, 0, 65536>, 0}, {"s4_stream_real_weave", l4s<96, 1, 65536>, 0}};  // (scan2 ABL 8|16 still stores the last tile: S is sized for 131072 columns)
     else if (D == 768)
       vs = {{"s4_full", l4<96, 0>, 0}, {"s4_full_ring3", l4<96, 128>, 0}, {"s4_no_stores_ring3", l4<96, 24 | 128>, 0},
             {"s4_no_stores", l4<96, 24>, 0}, {"s4_no_epi", l4<96, 1>, 0},
