@@ -139,7 +139,9 @@ constexpr int scan4_at(int s, int U) { return (s + 2 < U) ? s + 2 : U - 1; }
 // chain A: block B's epilogue (slices 0..E-1 from u = 2, after the accumulator tie), the
 // next tile's words (slice E), then the LDS-DMA pieces spaced SP u-steps apart (slices
 // E+1..): each DMA holds the wave's issue for ~20+ cycles; spread out rather than back to
-// back they cost 2-3 % less (staging still costs ~14 % of the kernel: the DMA issue itself).
+// back they cost 2-3 % less.  With their source offsets precomputed (no VALU per piece),
+// staging costs ~5 % of the d = 768 no-store scan (tools/scan4_probe: no_staging vs
+// no_stores); splitting them over both chains measured 4 % slower.
 constexpr int scan4_atA(int s, int U, int E, int pieces) {
   const int sp = (U - (E + 3)) / (pieces > 0 ? pieces : 1) > 1 ? (U - (E + 3)) / pieces : 1;
   const int u = s < E ? s + 2 : s == E ? E + 2 : E + 3 + (s - E - 1) * sp;
@@ -199,9 +201,10 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   const uint64_t clk0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;  // shader clock (word 7: cycles)
   stamp(0);
 
-  // LDS fragment addresses (scan2 layout: chunk (2u + h) ^ swz(r) of row r) and LDS-DMA
-  // source offsets are recomputed per use (a few VALU in the MFMA shadow) instead of held
-  // in registers: at d = 768 the two query blocks leave 128 VGPRs for everything else
+  // LDS fragment addresses (scan2 layout: chunk (2u + h) ^ swz(r) of row r): per-lane chunk
+  // offsets in registers on the interleaved schedule, one v_xor per read on the chained
+  // d = 768 one (whose two query blocks leave 128 VGPRs for everything else); the LDS-DMA
+  // source offsets are precomputed on both (below)
   const int swz = scan_swz<KU>(r);
   const int rrow = r * ROWB;
   const char* Xg = (const char*)a.X;
