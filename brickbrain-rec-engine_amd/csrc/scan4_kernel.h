@@ -425,22 +425,27 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
         any = __any(te >= sl.thr);
         if constexpr (ABL & 65536) {
           if (any) ep = s4_elig16(ok, ptile0, a.n_valid, h);  // (read by the woven compare / append slices)
-        } else if (any) {
-          // the eligibility, the compares and the appends under ONE uniform branch: a tile
-          // without hits (most of them) pays one branch per block instead of five (~22 cycles
-          // each, 12 % of the d = 384 streaming scan, tools/scan4_probe cfg 3); the hit
-          // bits from inline constants, four at a time (selects of 1 << (16 + g) made the
-          // compiler hold sixteen constants in VGPRs for the whole loop)
-          ep = s4_elig16(ok, ptile0, a.n_valid, h);
+        } else if (any || a.cand_pmax) {
+          // (and rank 0, slice 6 of the weave: a tile without hits in a search without a rank-0
+          // drop — semantic, CF — passes ONE branch)
+          if (a.cand_pmax) s4_rank0(a, p, ptile0, epw, h, tp, sl);
+          if (any) {
+            // the eligibility, the compares and the appends under ONE uniform branch: a tile
+            // without hits (most of them) pays one branch per block instead of five (~22 cycles
+            // each, 12 % of the d = 384 streaming scan, tools/scan4_probe cfg 3); the hit
+            // bits from inline constants, four at a time (selects of 1 << (16 + g) made the
+            // compiler hold sixteen constants in VGPRs for the whole loop)
+            ep = s4_elig16(ok, ptile0, a.n_valid, h);
 #pragma unroll
-          for (int g0 = 0; g0 < 16; g0 += 4) {
-            uint32_t m = 0;
+            for (int g0 = 0; g0 < 16; g0 += 4) {
+              uint32_t m = 0;
 #pragma unroll
-            for (int gg = 0; gg < 4; ++gg) m |= p[g0 + gg] >= sl.thrf ? 1u << gg : 0u;
-            asm volatile("" : "+v"(m));  // (keeps the shift out of the select constants)
-            ep |= m << (16 + g0);
+              for (int gg = 0; gg < 4; ++gg) m |= p[g0 + gg] >= sl.thrf ? 1u << gg : 0u;
+              asm volatile("" : "+v"(m));  // (keeps the shift out of the select constants)
+              ep |= m << (16 + g0);
+            }
+            if constexpr (!(ABL & 32)) s4_flush<ABL>(a, p, ptile0, h, (ep >> 16) & ep, sl, region(q), park);
           }
-          if constexpr (!(ABL & 32)) s4_flush<ABL>(a, p, ptile0, h, (ep >> 16) & ep, sl, region(q), park);
         }
       }
       if constexpr (PILOT) {
@@ -469,7 +474,8 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
         if constexpr ((ABL & 65536) && !(ABL & 32))
           if (any) s4_flush<ABL>(a, p, ptile0, h, (ep >> 16) & ep, sl, region(q), park);
       } else if constexpr (s == 6) {
-        if (a.cand_pmax) s4_rank0(a, p, ptile0, epw, h, tp, sl);
+        if constexpr (ABL & 65536)
+          if (a.cand_pmax) s4_rank0(a, p, ptile0, epw, h, tp, sl);
       }
     } else {
       if constexpr (s == 1) {

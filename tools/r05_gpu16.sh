@@ -1,5 +1,5 @@
 set -u
-T=r05merge
+T=r05r0
 mkdir -p gpurun_out/$T
 timeout -k 10 240 ./tools/scan4_probe 23 > gpurun_out/$T/probe.jsonl 2>&1 || exit $?
 timeout -k 10 600 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_scan4.py tests/test_gpu_configs.py -m gpu -x -q --timeout 240 --timeout-method thread -k "not c4_10M" > gpurun_out/$T/tests.log 2>&1; rc=$?
