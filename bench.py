@@ -405,15 +405,21 @@ def run_sharded(args, rank, world, local, dev):
             lo_r, hi_r = shard_bounds(n, world, r)
             if r == rank:
                 return lambda a, b: sh.local.get_rows(torch.arange(a - lo_r, b - lo_r, device=dev)).float().cpu().numpy()
-            xr = unit_rows_torch(hi_r - lo_r, d, 1234 + r, dev).to(torch.bfloat16).float().cpu().numpy()
-            return lambda a, b: xr[a - lo_r:b - lo_r]
+            def rows(a, b):   # lazily, one regenerated shard held at a time
+                if cache.get("r") != r:
+                    cache.clear()
+                    cache["x"] = unit_rows_torch(hi_r - lo_r, d, 1234 + r, dev).to(torch.bfloat16).float().cpu().numpy()
+                    cache["r"] = r
+                return cache["x"][a - lo_r:b - lo_r]
+            return rows
+        cache = {}
         owners = [(shard_bounds(n, world, r), shard_rows(r)) for r in range(world)]
 
         def get_chunk(a, b):   # global rows [a, b), possibly spanning shards
             parts = [f(max(a, lo_r), min(b, hi_r)) for (lo_r, hi_r), f in owners if max(a, lo_r) < min(b, hi_r)]
             return np.concatenate(parts, 0)
         out["cpu_baseline"] = cpu_full_scan(get_chunk, n, q[:64].cpu().numpy(), k)
-        del owners
+        del owners, cache
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()

@@ -20,13 +20,13 @@ BB_Q_OUT_KEYS = 1
 BB_Q_NULL_STREAM = 2
 BB_OPT_STREAM, BB_OPT_STREAM_MIN_ITEMS, BB_OPT_WORKSPACE_BYTES, BB_OPT_STREAM_REFINE, BB_OPT_RR_LISTS = 1, 2, 3, 4, 5
 BB_OPT_SMALL_BATCH = 6
-BB_OK, BB_E_ARG, BB_E_HIP, BB_E_STATE, BB_E_NOMEM = 0, -1, -2, -3, -4
+BB_OK, BB_E_ARG, BB_E_HIP, BB_E_STATE, BB_E_NOMEM, BB_E_HOSTSYNC = 0, -1, -2, -3, -4, -5
 
 # every entry point include/brickrec.h declares (checked by tests/test_abi.py)
 EXPORTS = ("bb_create", "bb_upload_items", "bb_upload_cf", "bb_upload_attrs", "bb_eval_mask",
            "bb_search", "bb_key_lens", "bb_finalize", "bb_set_profiling", "bb_get_profile", "bb_set_option",
            "bb_info", "bb_get_rows", "bb_create_view", "bb_destroy", "bb_last_error", "bb_abi_version",
-           "bb_plan_create", "bb_plan_launch", "bb_plan_destroy")
+           "bb_plan_create", "bb_plan_launch", "bb_plan_destroy", "bb_check_dual_scan_args")
 
 
 class BrickrecError(RuntimeError):
@@ -102,6 +102,7 @@ def load() -> C.CDLL:
             "bb_plan_create": ([P, C.POINTER(bb_query), C.POINTER(bb_result), C.POINTER(P)], C.c_int),
             "bb_plan_launch": ([P], C.c_int),
             "bb_plan_destroy": ([P], C.c_int),
+            "bb_check_dual_scan_args": ([C.c_int64], C.c_int),
             "bb_last_error": ([], C.c_char_p),
             "bb_abi_version": ([], C.c_int),
         }

@@ -79,6 +79,8 @@ class _Plan:
     (bb_plan_launch).  It holds its inputs, outputs and index alive; close() (or garbage
     collection, or closing the index) destroys the plan and its private view."""
 
+    is_plan = True  # run() replays a bb_plan (the bb_search closure says False)
+
     def __init__(self, lib, handle, root, keep):
         self._lib, self._p, self._root, self._keep = lib, handle, root, keep
         self._launch = lib.bb_plan_launch
@@ -339,7 +341,10 @@ class ItemIndex:
         torch CUDA tensors of the right dtypes; returns (run, outputs): each run() searches
         the inputs' current contents into the same outputs.  With plan=True (default) run is a
         bb_plan (include/brickrec.h): the host logic ran once, run() replays the launches; with
-        plan=False (or a search the plan refuses) run() calls bb_search."""
+        plan=False, or a search that synchronises with the host mid-way (bb_plan_create's
+        BB_E_HOSTSYNC: the streaming top-K), run() calls bb_search.  run.is_plan says which.
+        Any other plan refusal raises.  A plan may be called from several threads (the C-ABI
+        serialises its launches)."""
         import torch
         first = next(x for x in (q_rows, q_items, q_cf) if x is not None)
         dev, B = first.device, int(first.shape[0])
@@ -361,7 +366,7 @@ class ItemIndex:
         if plan:
             # bb_plan_create: the host side of the search runs once; each call replays its
             # launches.  Searches that synchronise with the host (the streaming top-K) refuse a
-            # plan (BB_E_STATE) and keep the bb_search call below.
+            # plan (BB_E_HOSTSYNC) and keep the bb_search call below; nothing else falls back.
             root = getattr(self, "_base", None) or self
             ph = C.c_void_p()
             with root._mu, self._mu:
@@ -371,7 +376,7 @@ class ItemIndex:
             if rc == 0:
                 p = _Plan(self._lib, ph, root, (keep, q, res, self))
                 return p, out
-            if rc != L.BB_E_STATE:
+            if rc != L.BB_E_HOSTSYNC:
                 L.check(rc, "bb_plan_create")
         fn, h, qp, rp = self._lib.bb_search, self._h, C.byref(q), C.byref(res)
 
@@ -380,6 +385,7 @@ class ItemIndex:
             if rc:
                 L.check(rc, "bb_search")
         run._keep = (keep, q, res, self)  # buffers, structs and the index handle live as long as the closure
+        run.is_plan = False
         return run, out
 
     # ------------------------------------------------------------------ sharded search

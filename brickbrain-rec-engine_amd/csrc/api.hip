@@ -98,9 +98,10 @@ bool live_del(const void* p) {
   std::lock_guard<std::mutex> lk(g_live_mu);
   return g_live.erase(p) != 0;
 }
-bool live_has(const void* p) {
+template <typename H>
+bool live_has_magic(const H* p, uint64_t magic) {
   std::lock_guard<std::mutex> lk(g_live_mu);
-  return g_live.count(p) != 0;
+  return g_live.count(p) != 0 && p->magic == magic;
 }
 
 }  // namespace
@@ -174,6 +175,13 @@ struct bb_plan {
   bb_index* view = nullptr;
   int device = 0;
   hipStream_t s = nullptr;
+  // launches of one plan from several threads are serialised by mu (two replays'
+  // launches interleaved on one stream would let one overwrite the other's scratch between
+  // producer and consumer); `done` is recorded after each replay, so destroy waits for the
+  // plan's own work only (the stream may be the caller's, gone by then: the event stays valid)
+  std::mutex mu;
+  hipEvent_t done = nullptr;
+  bool launched = false;
   std::vector<bb::CapturedOp> ops;
   std::vector<std::vector<void*>> argv;  // per launch: pointers into its argument blob
 };
@@ -181,16 +189,12 @@ struct bb_plan {
 namespace {
 
 // Handle checks of the entry points (see g_live above).
+// The magic word is read while g_live_mu is held (a destroy removes the handle under the same
+// lock before it frees anything).
 int check_index(const bb_index* x, const char* fn) {
   if (!x) return fail(BB_E_ARG, std::string(fn) + ": null index");
-  if (!live_has(x) || x->magic != kIndexMagic)
+  if (!live_has_magic(x, kIndexMagic))
     return fail(BB_E_ARG, std::string(fn) + ": stale or foreign index handle (destroyed, or not from bb_create)");
-  return BB_OK;
-}
-int check_plan(const bb_plan* p, const char* fn) {
-  if (!p) return fail(BB_E_ARG, std::string(fn) + ": null plan");
-  if (!live_has(p) || p->magic != kPlanMagic)
-    return fail(BB_E_ARG, std::string(fn) + ": stale or foreign plan handle (destroyed, or not from bb_plan_create)");
   return BB_OK;
 }
 #define BB_CHECK_INDEX(x, fn)                \
@@ -217,7 +221,7 @@ int s_memset(void* p, int v, size_t bytes, hipStream_t s) {
 }
 int s_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
   if (tl_capture) {
-    if (kind != hipMemcpyDeviceToDevice) return fail(BB_E_STATE, "bb_plan_create: the search copies to the host");
+    if (kind != hipMemcpyDeviceToDevice) return fail(BB_E_HOSTSYNC, "bb_plan_create: the search copies to the host");
     CapturedOp op;
     op.kind = 2;
     op.dst = dst;
@@ -243,7 +247,7 @@ hipError_t host_wait(hipStream_t s) {
 
 int s_sync(hipStream_t s) {
   if (tl_capture)
-    return fail(BB_E_STATE, "bb_plan_create: this search synchronises with the host (the streaming top-K of a large "
+    return fail(BB_E_HOSTSYNC, "bb_plan_create: this search synchronises with the host (the streaming top-K of a large "
                             "index): use bb_search");
   BB_HIP(host_wait(s));
   return BB_OK;
@@ -451,12 +455,17 @@ int bb_create_view(bb_index* b, bb_index** out) {
 
 int bb_destroy(bb_index* x) {
   if (!x) return BB_OK;
-  BB_CHECK_INDEX(x, "bb_destroy");
+  // removal from the live set is the point of truth: of two concurrent destroys
+  // one removes the handle and the other fails here without touching it
+  if (!live_del(x))
+    return fail(BB_E_ARG, "bb_destroy: stale or foreign index handle (destroyed, or not from bb_create)");
   {
     std::lock_guard<std::mutex> lk(x->mu);  // bb_create_view counts views under it
-    if (x->n_views > 0) return fail(BB_E_STATE, "bb_destroy: destroy the index's views (and plans) first");
+    if (x->n_views > 0) {
+      live_add(x);
+      return fail(BB_E_STATE, "bb_destroy: destroy the index's views (and plans) first");
+    }
   }
-  live_del(x);
   {
     DeviceGuard g(x->device);
     // a view's kernels read its base's rows: they finish before the base may be destroyed
@@ -935,7 +944,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     SqArgs a0 = side_args(0);
     SqArgs a1 = hyb ? side_args(1) : a0;
     // BB_SQ_TRACE (probe runs): phase stamps of side 0's pass workgroups and merge rows
-    static const bool sq_trace = ab_env("BB_SQ_TRACE") != nullptr;
+    static const bool sq_trace = kProbes && ab_env("BB_SQ_TRACE") != nullptr;
     if (sq_trace) {
       if ((rc = x->trace.ensure((size_t)(nwg + B) * 8 * 8))) return rc;
       BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)(nwg + B) * 64, s));
@@ -1391,10 +1400,12 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
           if (dual && side == 0) {
             ga_dual0 = ga;  // launched with side 1's
           } else if (dual) {
+            const char* why = nullptr;
+            if (!scan4_dual_args_ok(ga_dual0, ga, &why)) return fail(BB_E_ARG, std::string("hybrid dual scan: ") + why);
             if ((rc = timed(x, K_GEMM, s, [&] { return launch_scan4_dual(ga_dual0, ga, s); }))) return rc;
           } else {
             // BB_SCAN_TRACE (probe runs): phase stamps of the list scan's workgroups (scan4)
-            static const bool scan_trace = ab_env("BB_SCAN_TRACE") != nullptr;
+            static const bool scan_trace = kProbes && ab_env("BB_SCAN_TRACE") != nullptr;
             const bool tr = scan_trace && ga.lists && scan4_used(BF16, bpad);
             if (tr) {
               if ((rc = x->trace.ensure((size_t)4096 * 64))) return rc;
@@ -1563,7 +1574,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
             continue;
           }
           const bool both = q->mode == BB_MODE_HYBRID && side == 1 && list_c;
-          static const bool ls_trace = ab_env("BB_SELECT_TRACE") != nullptr;
+          static const bool ls_trace = kProbes && ab_env("BB_SELECT_TRACE") != nullptr;
           if (ls_trace) {  // probe runs: phase stamps of side 0's rows (16 words per row)
             if ((rc = x->trace.ensure((size_t)bc * 16 * 8))) return rc;
             BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 128, s));
@@ -1619,7 +1630,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         }
         // BB_SELECT_TRACE (probe runs): per-phase s_memrealtime stamps of every query row,
         // averaged over the rows and printed to stderr
-        static const bool sel_trace = ab_env("BB_SELECT_TRACE") != nullptr;
+        static const bool sel_trace = kProbes && ab_env("BB_SELECT_TRACE") != nullptr;
         if (sel_trace) {
           if ((rc = x->trace.ensure((size_t)bc * 8 * 8))) return rc;
           BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 64, s));
@@ -1737,7 +1748,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     fa.ids = o_id + (size_t)b0 * q->k;
     fa.counts = o_cnt ? o_cnt + b0 : nullptr;
     fa.n_rows = bc;
-    static const bool fin_trace = ab_env("BB_SELECT_TRACE") != nullptr;
+    static const bool fin_trace = kProbes && ab_env("BB_SELECT_TRACE") != nullptr;
     if (fin_trace) {
       if ((rc = x->trace.ensure((size_t)bc * 8 * 8))) return rc;
       BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 64, s));
@@ -1771,7 +1782,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     if (tl_capture) return s_sync(s);  // (fails the plan: the host reads the flag)
     BB_HIP(host_wait(s));
     const uint32_t overflowed = *(volatile uint32_t*)x->ovf_host;
-    if (overflowed && ab_env("BB_STREAM_DEBUG")) {
+    if (kProbes && overflowed && ab_env("BB_STREAM_DEBUG")) {
       int rg, cap;
       const int bpl = (int)pad_rows(B - (B - 1) / Bc * Bc);
       stream_geom(bpl, refine ? 1 : 0, rg, cap);
@@ -1951,6 +1962,30 @@ int bb_get_profile(bb_index* x, bb_profile* out) {
 }
 
 // ---- prepared searches ----------------------------------------------------------------------
+// Diagnostics: the hybrid dual scan's shape rules on a configs[2]-shaped argument pair whose
+// item row stride is `ldx` (both sides); no device call (the 24-bit DMA
+// offset guard, tested on the CPU).
+int bb_check_dual_scan_args(int64_t ldx) {
+  GemmArgs a0{}, a1{};
+  static float h[1];
+  static char lists[16];
+  for (GemmArgs* g : {&a0, &a1}) {
+    g->ldx = ldx;
+    g->Mpad = 1024;
+    g->Ncols = 25216;
+    g->s_h = h;
+    g->f16 = 1;
+    g->lists = (decltype(g->lists))lists;
+    g->l_period = 4;
+    g->l_np = 2;
+  }
+  a0.Kpad = 384;
+  a1.Kpad = 64;
+  const char* why = nullptr;
+  if (!scan4_dual_args_ok(a0, a1, &why)) return fail(BB_E_ARG, std::string("bb_check_dual_scan_args: ") + why);
+  return BB_OK;
+}
+
 int bb_plan_create(bb_index* x, const bb_query* q, const bb_result* res, bb_plan** out) {
   BB_CHECK_INDEX(x, "bb_plan_create");
   if (!q || !res || !out) return fail(BB_E_ARG, "bb_plan_create: null argument");
@@ -1988,7 +2023,12 @@ int bb_plan_create(bb_index* x, const bb_query* q, const bb_result* res, bb_plan
     delete p;
     (void)bb_destroy(v);
     g_err = msg;
-    return rc == kRetrySlab ? BB_E_STATE : rc;
+    return rc == kRetrySlab ? BB_E_HOSTSYNC : rc;
+  }
+  if (hipEventCreateWithFlags(&p->done, hipEventDisableTiming) != hipSuccess) {
+    delete p;
+    (void)bb_destroy(v);
+    return fail(BB_E_HIP, "bb_plan_create: hipEventCreateWithFlags failed");
   }
   p->argv.resize(p->ops.size());
   for (size_t i = 0; i < p->ops.size(); ++i)
@@ -1999,8 +2039,16 @@ int bb_plan_create(bb_index* x, const bb_query* q, const bb_result* res, bb_plan
 }
 
 int bb_plan_launch(bb_plan* p) {
-  const int rc0 = check_plan(p, "bb_plan_launch");
-  if (rc0) return rc0;
+  if (!p) return fail(BB_E_ARG, "bb_plan_launch: null plan");
+  std::unique_lock<std::mutex> pl;
+  {
+    // the plan's lock is taken while the live set says the plan exists, so a destroy (which
+    // removes it from the set first, then takes the plan's lock) waits for this launch
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    if (!g_live.count(p) || p->magic != kPlanMagic)
+      return fail(BB_E_ARG, "bb_plan_launch: stale or foreign plan handle (destroyed, or not from bb_plan_create)");
+    pl = std::unique_lock<std::mutex>(p->mu);
+  }
   int cur = -1;
   if (hipGetDevice(&cur) != hipSuccess || cur != p->device) BB_HIP(hipSetDevice(p->device));
   for (size_t i = 0; i < p->ops.size(); ++i) {
@@ -2017,19 +2065,24 @@ int bb_plan_launch(bb_plan* p) {
       return fail(BB_E_HIP, std::string("bb_plan_launch: ") + hipGetErrorString(e));
     }
   }
+  const hipError_t e = hipEventRecord(p->done, p->s);
+  p->launched = p->launched || e == hipSuccess;
   if (cur >= 0 && cur != p->device) (void)hipSetDevice(cur);
+  if (e != hipSuccess) return fail(BB_E_HIP, std::string("bb_plan_launch: hipEventRecord: ") + hipGetErrorString(e));
   return BB_OK;
 }
 
 int bb_plan_destroy(bb_plan* p) {
   if (!p) return BB_OK;
-  const int rc0 = check_plan(p, "bb_plan_destroy");
-  if (rc0) return rc0;
-  live_del(p);
+  if (!live_del(p))
+    return fail(BB_E_ARG, "bb_plan_destroy: stale or foreign plan handle (destroyed, or not from bb_plan_create)");
   {
+    std::lock_guard<std::mutex> pl(p->mu);  // a launch that passed its check finishes enqueueing
     DeviceGuard g(p->device);
-    // the replays ran on the caller's stream, which may be gone by now: wait for the device
-    (void)hipDeviceSynchronize();
+    // the replays ran on the caller's stream, which may be gone by now: wait for the last
+    // replay's event (recorded after its launches), not for the whole device
+    if (p->launched) (void)hipEventSynchronize(p->done);
+    (void)hipEventDestroy(p->done);
   }
   const int rc = bb_destroy(p->view);
   p->magic = 0;

@@ -18,6 +18,13 @@ inline const char* ab_env(const char* name) {
   static const bool on = std::getenv("BB_AB") != nullptr;
   return on ? std::getenv(name) : nullptr;
 }
+// Probe builds only (make PROBES=1): the phase-stamp trace printers (BB_SQ_TRACE,
+// BB_SCAN_TRACE, BB_SELECT_TRACE, BB_STREAM_DEBUG).  The shipped library is built with
+// kProbes = false, so each printer's guard is a constant and the code is not emitted.
+#ifndef BB_PROBES
+#define BB_PROBES 0
+#endif
+constexpr bool kProbes = BB_PROBES != 0;
 
 // ---- item ordering keys ------------------------------------------------------------------
 // A candidate is one u64: high word = order-preserving image of the fp32 score, low word =
@@ -456,6 +463,7 @@ int scan_chunks(int dtype, int Mpad, int tiles, bool split, int list_ku = 0);
 bool launch_scan4(const GemmArgs& a, int ku, hipStream_t s);  // scan4_used(BF16, a.Mpad) shapes
 int scan4_pilot_m(int kpad);  // GemmArgs.pilot_m of a kScanPilot scan4 launch
 bool scan4_dual_supported(int ku0, int ku1);
+bool scan4_dual_args_ok(const GemmArgs& a0, const GemmArgs& a1, const char** why);
 hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s);  // hybrid, int16 image
 hipError_t launch_scan3(const GemmArgs& a, hipStream_t s);  // X = item planes, Q = q3f image
 hipError_t launch_split_planes(const float* src, int64_t n, int64_t ld, uint16_t* dst, hipStream_t s);

@@ -51,15 +51,30 @@ static bool launch_dual_k1(const GemmArgs& a0, const GemmArgs& a1, int ku1, hipS
 bool scan4_dual_supported(int ku0, int ku1) {
   return (ku0 == 24 || ku0 == 32 || ku0 == 48 || ku0 == 64) && (ku1 == 8 || ku1 == 16);
 }
+// The dual launcher's shape rules; *why names the first one broken (nullptr: all hold).
+bool scan4_dual_args_ok(const GemmArgs& a0, const GemmArgs& a1, const char** why) {
+  const int ku0 = a0.Kpad * 2 / 16, ku1 = a1.Kpad * 2 / 16;
+  const char* w = nullptr;
+  if (a0.ldx <= 0 || a0.ldx >= (int64_t(1) << 23) || a1.ldx <= 0 || a1.ldx >= (int64_t(1) << 23))
+    w = "item row stride outside (0, 2^23): the LDS-DMA source offsets are 24-bit (scan4_kernel.h)";
+  else if (!scan4_dual_supported(ku0, ku1))
+    w = "row widths outside the dual instances (content 192..512, CF up to 128)";
+  else if (!a0.s_h || !a1.s_h || !a0.f16 || !a1.f16 || a0.cand || a1.cand || !scan4_used(BF16, a0.Mpad) ||
+           a0.Mpad != a1.Mpad)
+    w = "not an f16 re-rank scan pair of equal query rows";
+  else if (!a0.lists != !a1.lists || (a0.lists && (a0.l_period <= 0 || a0.l_np <= 0 || a1.l_period <= 0 || a1.l_np <= 0)))
+    w = "list geometry";
+  else if (a0.Ncols % 32 || a1.Ncols % 32 || (a0.slab_start & 31) || (a1.slab_start & 31))
+    w = "slab not tile-aligned";
+  else if (a0.q_ids || a0.q_src || a0.q_istats || a1.q_ids || a1.q_src || a1.q_istats)
+    w = "fused query prologue";
+  if (why) *why = w;
+  return w == nullptr;
+}
+
 hipError_t launch_scan4_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
   const int ku0 = a0.Kpad * 2 / 16, ku1 = a1.Kpad * 2 / 16;
-  if (!scan4_dual_supported(ku0, ku1) || !a0.s_h || !a1.s_h || !a0.f16 || !a1.f16 || a0.cand || a1.cand ||
-      !scan4_used(BF16, a0.Mpad) ||
-      !a0.lists != !a1.lists || (a0.lists && (a0.l_period <= 0 || a0.l_np <= 0 || a1.l_period <= 0 || a1.l_np <= 0)) ||
-      a0.Mpad != a1.Mpad || a0.Ncols % 32 || a1.Ncols % 32 || (a0.slab_start & 31) || (a1.slab_start & 31) || a0.q_ids ||
-      a0.q_src || a0.q_istats || a1.q_ids || a1.q_src || a1.q_istats || a0.ldx <= 0 || a0.ldx >= (int64_t(1) << 23) ||
-      a1.ldx <= 0 || a1.ldx >= (int64_t(1) << 23))  // 24-bit DMA offsets (scan4_kernel.h)
-    return hipErrorInvalidValue;
+  if (!scan4_dual_args_ok(a0, a1, nullptr)) return hipErrorInvalidValue;
   bool ok = false;
   switch (ku0) {
     case 24: ok = launch_dual_k1<24>(a0, a1, ku1, s); break;

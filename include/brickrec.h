@@ -38,6 +38,7 @@ extern "C" {
 #define BB_E_HIP (-2)      /* HIP runtime error (message in bb_last_error) */
 #define BB_E_STATE (-3)    /* call out of order (e.g. search before upload) */
 #define BB_E_NOMEM (-4)    /* device allocation failed */
+#define BB_E_HOSTSYNC (-5) /* bb_plan_create: the search synchronises with the host mid-way (no plan: use bb_search) */
 
 /* element types */
 #define BB_F32 0
@@ -242,16 +243,30 @@ int bb_create_view(bb_index* base, bb_index** out);
  * The plan owns a private view of the index (its own workspace): plans never race with
  * bb_search or with each other on scratch buffers, and the index accepts no upload while a
  * plan exists (BB_E_STATE, as with views).  Searches that synchronise with the host (the
- * streaming top-K of indexes >= BB_OPT_STREAM_MIN_ITEMS rows) return BB_E_STATE: use
- * bb_search for those.  bb_plan_destroy waits for the device before releasing the view. */
+ * streaming top-K of indexes >= BB_OPT_STREAM_MIN_ITEMS rows) return BB_E_HOSTSYNC: use
+ * bb_search for those; any other refusal is an error.  One plan may be launched from several
+ * threads: bb_plan_launch holds the plan's lock while it enqueues, so two replays never
+ * interleave their launches on the plan's workspace (they still share it: the second replay
+ * queues behind the first on the stream).  bb_plan_destroy waits for the plan's last replay
+ * (an event recorded after each launch), not for the whole device, then releases the view. */
 typedef struct bb_plan bb_plan;
 int bb_plan_create(bb_index* idx, const bb_query* q, const bb_result* res, bb_plan** out);
 int bb_plan_launch(bb_plan* plan);
 int bb_plan_destroy(bb_plan* plan);
 
+/* Diagnostics (no device call): BB_OK when the hybrid dual list scan accepts a configs[2]-shaped
+ * argument pair (1,024 query rows, 25,216 items, f16 content rows 384 wide, CF 64) with item row
+ * stride `ldx`, else BB_E_ARG naming the broken rule — the scan's LDS-DMA source offsets are 24-bit,
+ * so a stride >= 2^23 is refused before any launch instead of faulting. */
+int bb_check_dual_scan_args(int64_t ldx);
+
 int bb_info(bb_index* idx, int64_t* n_items, int32_t* d, int32_t* d_pad, int32_t* r);
 /* Handles are checked by every entry point: a destroyed, foreign or corrupted bb_index /
- * bb_plan pointer returns BB_E_ARG with a message in bb_last_error(), never a crash. */
+ * bb_plan pointer returns BB_E_ARG with a message in bb_last_error(), never a crash.  A handle
+ * is invalid from the moment its destroy call begins (removal from the live set is the point
+ * of truth: of two concurrent destroys of one handle, one succeeds and the other returns
+ * BB_E_ARG), even if its address is later reused by a new handle; calling other entry points
+ * on a handle while another thread destroys it is misuse. */
 int bb_destroy(bb_index* idx);
 const char* bb_last_error(void);
 int bb_abi_version(void);

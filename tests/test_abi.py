@@ -142,3 +142,17 @@ def test_stale_and_foreign_handles_are_errors():
             assert b"stale or foreign" in lib.bb_last_error(), name
     # NULL stays "nothing to destroy"
     assert lib.bb_destroy(None) == L.BB_OK and lib.bb_plan_destroy(None) == L.BB_OK
+
+
+def test_dual_scan_refuses_24bit_dma_overflow():
+    """scan4's LDS-DMA source offsets are 24-bit, so the hybrid dual list
+    scan's launcher refuses an item row stride >= 2^23 (BB_E_ARG, the rule named in
+    bb_last_error) before any launch instead of faulting; bb_search maps the same check to
+    BB_E_ARG.  Runs the launcher's own rule set (scan4_dual_args_ok) on the CPU."""
+    from brickrec import _lib as L
+    lib = L.load()
+    assert lib.bb_check_dual_scan_args(384) == L.BB_OK            # configs[2]'s stride
+    assert lib.bb_check_dual_scan_args((1 << 23) - 1) == L.BB_OK
+    for bad in (1 << 23, (1 << 23) + 384, 1 << 40, 0, -8):
+        assert lib.bb_check_dual_scan_args(bad) == L.BB_E_ARG, bad
+        assert b"24-bit" in lib.bb_last_error()

@@ -454,7 +454,8 @@ def test_plan_replays_the_search(brickrec, B):
 
 def test_plan_refused_on_streaming_falls_back(brickrec):
     """A streaming search reads its overflow flag on the host: bb_plan_create refuses it
-    (BB_E_STATE) and prepared_search keeps the bb_search call — same results."""
+    (BB_E_HOSTSYNC, a code of its own: ADVICE r05) and prepared_search keeps the bb_search
+    call — same results, and run.is_plan says so."""
     import torch
     n, d, B, k = 3000, 128, 40, 10      # B > 16: not the small-batch path
     x = R.unit_rows(n, d, 31)
@@ -464,7 +465,7 @@ def test_plan_refused_on_streaming_falls_back(brickrec):
         idx.set_option("stream", 1)
         q = torch.from_numpy(R.unit_rows(B, d, 32)).cuda()
         run, out = idx.prepared_search("semantic", k, q_rows=q)
-        assert type(run).__name__ != "_Plan"
+        assert type(run).__name__ != "_Plan" and run.is_plan is False
         run()
         torch.cuda.synchronize()
         ref = idx.search("semantic", k, q_rows=q.cpu().numpy())
@@ -493,3 +494,50 @@ def test_destroyed_handle_is_an_error(brickrec):
     assert lib.bb_search(h, C.byref(qs), C.byref(res)) == L.BB_E_ARG
     assert b"stale or foreign" in lib.bb_last_error()
     assert lib.bb_destroy(h) == L.BB_E_ARG
+
+
+def test_plan_launched_from_two_threads(brickrec):
+    """bb_plan_launch holds the plan's lock while it enqueues, so two
+    threads replaying ONE plan never interleave their launches on its workspace.  Both threads
+    replay the list-path plan (B = 256: prep -> scan -> select, three dependent launches over
+    shared scratch) 40 times each; the results equal bb_search's bit for bit.  Then a second
+    destroy of the same plan is an error, not a double free."""
+    import ctypes as C
+    import threading
+    import torch
+    from brickrec import _lib as L
+    dev = torch.device("cuda", 0)
+    n, d, B, k = 25216, 384, 256, 50
+    x = R.unit_rows(n, d, 77)
+    qn = R.unit_rows(B, d, 78)
+    idx = brickrec.ItemIndex(dtype="f32")
+    try:
+        idx.upload_items(x, prenormalized=True)
+        q = torch.from_numpy(qn).to(dev)
+        run, out = idx.prepared_search("semantic", k, q_rows=q)
+        assert run.is_plan
+        errs = []
+
+        def worker():
+            try:
+                for _ in range(40):
+                    run()
+            except Exception as e:   # pragma: no cover - reported below
+                errs.append(e)
+        ts = [threading.Thread(target=worker) for _ in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        torch.cuda.synchronize()
+        assert not errs, errs
+        ref = idx.search("semantic", k, q_rows=qn)
+        assert np.array_equal(out[1].cpu().numpy(), ref[1])
+        assert np.array_equal(out[0].cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
+        lib = L.load()
+        p = run._p
+        run.close()
+        assert lib.bb_plan_destroy(p) == L.BB_E_ARG      # already destroyed
+        assert b"stale or foreign" in lib.bb_last_error()
+    finally:
+        idx.close()
