@@ -19,7 +19,8 @@ BB_MODE_SEMANTIC, BB_MODE_SIMILAR, BB_MODE_CF, BB_MODE_HYBRID = 0, 1, 2, 3
 BB_Q_OUT_KEYS = 1
 BB_Q_NULL_STREAM = 2
 BB_OPT_STREAM, BB_OPT_STREAM_MIN_ITEMS, BB_OPT_WORKSPACE_BYTES, BB_OPT_STREAM_REFINE, BB_OPT_RR_LISTS = 1, 2, 3, 4, 5
-BB_OPT_SMALL_BATCH = 6
+BB_OPT_SMALL_BATCH, BB_OPT_PREFILTER = 6, 7
+ABI_VERSION = 2   # include/brickrec.h BB_ABI_VERSION (2: bb_query.mask_count)
 BB_OK, BB_E_ARG, BB_E_HIP, BB_E_STATE, BB_E_NOMEM, BB_E_HOSTSYNC = 0, -1, -2, -3, -4, -5
 
 # every entry point include/brickrec.h declares (checked by tests/test_abi.py)
@@ -53,7 +54,7 @@ class bb_query(C.Structure):
                 ("q_cf", C.c_void_p), ("q_cf_dtype", C.c_int32),
                 ("mask_bits", C.c_void_p), ("excl_bits", C.c_void_p),
                 ("w_content", C.c_double), ("w_cf", C.c_double),
-                ("stream", C.c_void_p)]
+                ("stream", C.c_void_p), ("mask_count", C.c_int64)]
 
 
 class bb_result(C.Structure):
@@ -110,8 +111,8 @@ def load() -> C.CDLL:
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res
-        if lib.bb_abi_version() != 1:
-            raise BrickrecError(f"libbrickrec ABI {lib.bb_abi_version()} != 1")
+        if lib.bb_abi_version() != ABI_VERSION:
+            raise BrickrecError(f"libbrickrec ABI {lib.bb_abi_version()} != {ABI_VERSION}")
         _lib = lib
         return lib
 

@@ -250,23 +250,26 @@ class ItemIndex:
 
     # ------------------------------------------------------------------ search
     def _query(self, mode, k, B, k_side, where, q_rows, q_dtype, q_items, q_cf, q_cf_dtype, mask,
-               excl, w_content, w_cf, stream, flags):
+               excl, w_content, w_cf, stream, flags, mask_count=0):
         return L.bb_query(MODES[mode] if isinstance(mode, str) else mode, flags, B, k, k_side, where,
                           q_rows, q_dtype, q_items, q_cf, q_cf_dtype, mask, excl,
-                          float(w_content), float(w_cf), stream)
+                          float(w_content), float(w_cf), stream, int(mask_count or 0))
 
     def search(self, mode: str, k: int, *, q_rows=None, q_items=None, q_cf=None, mask=None,
                excl=None, k_side: int = 0, w_content: float = 0.4, w_cf: float = 0.6,
-               stream=None, out=None):
+               stream=None, out=None, mask_count: int = 0):
         """Batched top-k.  Returns (scores [B,k] f32, ids [B,k] i64, counts [B] i32).
 
         mask: bool [n] (or uint32 words) — items allowed (valid_set_filter); excl: bool
         [B, n] (or words) — per-query excluded items (CF: rated).  Torch CUDA inputs run
-        fully asynchronously on `stream` (default: torch's current stream)."""
+        fully asynchronously on `stream` (default: torch's current stream).  mask_count: the
+        number of allowed items of a device (torch int32 words) mask, when known — the
+        length of the reference's valid_set_nums; host and bool masks are counted here or
+        by the library (bb_query.mask_count, constraint-first search)."""
         first = next(x for x in (q_rows, q_items, q_cf) if x is not None)
         if _is_torch(first):
             return self._search_torch(mode, k, q_rows, q_items, q_cf, mask, excl, k_side, w_content,
-                                      w_cf, stream, out)
+                                      w_cf, stream, out, mask_count)
         B = int(np.asarray(first).shape[0])
         keep = []
 
@@ -299,7 +302,7 @@ class ItemIndex:
         return scores, ids, counts
 
     def _search_torch(self, mode, k, q_rows, q_items, q_cf, mask, excl, k_side, w_content, w_cf,
-                      stream, out):
+                      stream, out, mask_count=0):
         import torch
         first = next(x for x in (q_rows, q_items, q_cf) if x is not None)
         dev = first.device
@@ -315,7 +318,9 @@ class ItemIndex:
             return t.data_ptr()
 
         if mask is not None and mask.dtype == torch.bool:
-            mask = torch.from_numpy(bits_from_bool(mask.cpu().numpy()).view(np.int32)).to(dev)
+            mb = mask.cpu().numpy()
+            mask_count = int(np.count_nonzero(mb[: self.n_items]))
+            mask = torch.from_numpy(bits_from_bool(mb).view(np.int32)).to(dev)
         if excl is not None and excl.dtype == torch.bool:
             excl = torch.from_numpy(bits_from_bool(excl.cpu().numpy()).view(np.int32)).to(dev)
         if out is None:
@@ -327,7 +332,7 @@ class ItemIndex:
                         ptr(q_rows), _torch_dtype_code(q_rows) if q_rows is not None else 0,
                         ptr(q_items, torch.int64),
                         ptr(q_cf), _torch_dtype_code(q_cf) if q_cf is not None else 0,
-                        ptr(mask), ptr(excl), w_content, w_cf, s.cuda_stream, _null(s))
+                        ptr(mask), ptr(excl), w_content, w_cf, s.cuda_stream, _null(s), mask_count)
         res = L.bb_result(out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), L.BB_DEVICE,
                           None, None)
         with self._mu:
@@ -336,7 +341,7 @@ class ItemIndex:
 
     def prepared_search(self, mode: str, k: int, *, q_rows=None, q_items=None, q_cf=None,
                         mask=None, excl=None, k_side: int = 0, w_content=0.4, w_cf=0.6,
-                        stream=None, plan: bool = True):
+                        stream=None, plan: bool = True, mask_count: int = 0):
         """A repeated device-resident search (the serving loop; bench).  All inputs must be
         torch CUDA tensors of the right dtypes; returns (run, outputs): each run() searches
         the inputs' current contents into the same outputs.  With plan=True (default) run is a
@@ -361,7 +366,7 @@ class ItemIndex:
                         _torch_dtype_code(q_cf) if q_cf is not None else 0,
                         mask.data_ptr() if mask is not None else None,
                         excl.data_ptr() if excl is not None else None, w_content, w_cf,
-                        s.cuda_stream, _null(s))
+                        s.cuda_stream, _null(s), mask_count)
         res = L.bb_result(out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), L.BB_DEVICE, None, None)
         if plan:
             # bb_plan_create: the host side of the search runs once; each call replays its
@@ -524,7 +529,8 @@ class ItemIndex:
         "small_batch" (-1 auto / 0 off: the one-pass exact search of batches of <= 16 rows)."""
         code = {"stream": L.BB_OPT_STREAM, "stream_min_items": L.BB_OPT_STREAM_MIN_ITEMS,
                 "workspace_bytes": L.BB_OPT_WORKSPACE_BYTES, "stream_refine": L.BB_OPT_STREAM_REFINE,
-                "rr_lists": L.BB_OPT_RR_LISTS, "small_batch": L.BB_OPT_SMALL_BATCH}[option]
+                "rr_lists": L.BB_OPT_RR_LISTS, "small_batch": L.BB_OPT_SMALL_BATCH,
+                "prefilter": L.BB_OPT_PREFILTER}[option]
         with self._mu:
             L.check(self._lib.bb_set_option(self._h, code, int(value)), "bb_set_option")
 

@@ -118,6 +118,7 @@ struct bb_index {
   int refine_opt = -1;                 // BB_OPT_STREAM_REFINE
   int lists_opt = -1;                  // BB_OPT_RR_LISTS
   int sq_opt = -1;                     // BB_OPT_SMALL_BATCH
+  int prefilter_opt = -1;              // BB_OPT_PREFILTER
   bb_index* base = nullptr;            // a view (bb_create_view): the handle owning the rows
   std::atomic<int> n_views{0};         // views of this handle still alive
   hipStream_t stream = nullptr;
@@ -156,6 +157,16 @@ struct bb_index {
   DevBuf lists, r0lists;  // bounded candidate lists of the list scans (list_epi.h), both sides
   DevBuf sq_top, sq_ptop, sq_ords;  // small-batch exact search (sq.hip)
   uint32_t* ovf_host = nullptr;  // pinned
+  // constraint-first search (compact.hip): the rank-0 key of every item's own row (its
+  // unmasked arg-max, :217; [n] = a zero row's), built at upload for f32 indexes of up to
+  // 65,536 rows, and the packed shadow index a selective mask's rows are gathered into
+  DevBuf r0key;
+  bool r0_ready = false;
+  bb_index* cx = nullptr;          // the shadow (owned; not a live handle)
+  bool shadow = false;             // this index is a shadow: no rank-0 drop, final ids via idmap
+  DevBuf idmap, cq_rows, cexcl0, cexcl1;  // shadow: position -> id, liked rows, exclusions
+  const uint32_t* cur_cexcl = nullptr;    // shadow: the content exclusions of this search
+  size_t filled_words = 0;                // shadow: words of ones / zeros filled
 
   bool prof = false;
   struct Pending {
@@ -187,6 +198,24 @@ struct bb_plan {
 };
 
 namespace {
+
+// Every device buffer and profiling event of a handle (bb_destroy; a shadow index's too).
+void free_buffers(bb_index* x) {
+  for (auto& p : x->pending) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  x->pending.clear();
+  for (DevBuf* b : {&x->items, &x->items_present, &x->ones, &x->zeros, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S, &x->tmax,
+                    &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
+                    &x->cand, &x->cand_cnt, &x->cand_pmax, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
+                    &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
+                    &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists, &x->pilot_top,
+                    &x->sq_top, &x->sq_ptop, &x->sq_ords, &x->r0key, &x->idmap, &x->cq_rows, &x->cexcl0, &x->cexcl1})
+    b->release();
+  if (x->ovf_host) (void)hipHostFree(x->ovf_host);
+  x->ovf_host = nullptr;
+}
 
 // Handle checks of the entry points (see g_live above).
 // The magic word is read while g_live_mu is held (a destroy removes the handle under the same
@@ -428,6 +457,8 @@ int bb_create_view(bb_index* b, bb_index** out) {
   x->refine_opt = b->refine_opt;
   x->lists_opt = b->lists_opt;
   x->sq_opt = b->sq_opt;
+  x->prefilter_opt = b->prefilter_opt;
+  x->r0_ready = b->r0_ready;
   x->n = b->n;
   x->Npad = b->Npad;
   x->d = b->d;
@@ -442,7 +473,8 @@ int bb_create_view(bb_index* b, bb_index** out) {
                   std::make_pair(&x->items3, &b->items3), std::make_pair(&x->cf3, &b->cf3),
                   std::make_pair(&x->items_bf, &b->items_bf), std::make_pair(&x->cf_bf, &b->cf_bf),
                   std::make_pair(&x->rr_stats, &b->rr_stats), std::make_pair(&x->parts, &b->parts),
-                  std::make_pair(&x->year, &b->year), std::make_pair(&x->theme, &b->theme)}) {
+                  std::make_pair(&x->year, &b->year), std::make_pair(&x->theme, &b->theme),
+                  std::make_pair(&x->r0key, &b->r0key)}) {
     pr.first->p = pr.second->p;
     pr.first->cap = pr.second->cap;
     pr.first->owned = false;
@@ -478,18 +510,12 @@ int bb_destroy(bb_index* x) {
   }
   {
     DeviceGuard g(x->device);
-    for (auto& p : x->pending) {
-      (void)hipEventDestroy(p.a);
-      (void)hipEventDestroy(p.b);
+    free_buffers(x);
+    if (x->cx) {  // the shadow's kernels ran on x's streams, synchronised above
+      free_buffers(x->cx);
+      delete x->cx;
+      x->cx = nullptr;
     }
-    for (DevBuf* b : {&x->items, &x->items_present, &x->ones, &x->zeros, &x->cf, &x->cf_present, &x->parts, &x->year, &x->theme, &x->qn, &x->qcf, &x->S, &x->tmax,
-                      &x->keys, &x->maxk, &x->stage_in, &x->out_sc, &x->out_id, &x->out_cnt, &x->tmp, &x->pilot, &x->list1, &x->max1,
-                      &x->cand, &x->cand_cnt, &x->cand_pmax, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
-                      &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
-                      &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists, &x->pilot_top,
-                      &x->sq_top, &x->sq_ptop, &x->sq_ords})
-      b->release();
-    if (x->ovf_host) (void)hipHostFree(x->ovf_host);
     if (x->has_last) (void)hipEventSynchronize(x->done);
     (void)hipEventDestroy(x->done);
     (void)hipStreamDestroy(x->stream);
@@ -606,6 +632,58 @@ static int make_rr(bb_index* x, DevBuf& rows, DevBuf& bf, int ld, int& ld_b, int
   return BB_OK;
 }
 
+}  // extern "C"
+
+namespace {
+int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_stream);
+
+// The rank-0 table of the constraint-first search (compact.hip): every item's own stored row
+// searched as a similar-sets query (k = 1, key lists out) over this index — its max key is
+// the arg-max of the unmasked ranking that get_similar_sets drops (:217), the same key the
+// full search's list select finds — plus one zero row (an id outside the index, as the
+// gather treats it).  Built once per upload; read by the packed searches of similar / hybrid
+// queries, whose packed rows no longer hold the unmasked ranking.
+int build_r0(bb_index* x) {
+  x->r0_ready = false;
+  const int64_t n = x->n, B = n + 1;
+  int rc;
+  if ((rc = x->r0key.ensure((size_t)B * 8))) return rc;
+  DevBuf ids, keys;
+  std::vector<int64_t> h((size_t)B);
+  for (int64_t i = 0; i < n; ++i) h[(size_t)i] = x->id_offset + i;
+  h[(size_t)n] = x->id_offset - 1;
+  bb_query q{};
+  q.mode = BB_MODE_SIMILAR;
+  q.flags = BB_Q_OUT_KEYS;
+  q.B = (int32_t)B;
+  q.k = 1;
+  q.where = BB_DEVICE;
+  q.stream = x->stream;
+  bb_result r{};
+  r.where = BB_DEVICE;
+  r.max_keys = (uint64_t*)x->r0key.p;
+  if ((rc = ids.ensure((size_t)B * 8)) || (rc = keys.ensure((size_t)B * 2 * 8))) return rc;
+  q.q_items = (const int64_t*)ids.p;
+  r.keys = (uint64_t*)keys.p;
+  hipError_t e = hipMemcpyAsync(ids.p, h.data(), (size_t)B * 8, hipMemcpyHostToDevice, x->stream);
+  if (e == hipSuccess) {
+    const bool prof = x->prof;  // (not a caller's search: nothing joins the profile)
+    x->prof = false;
+    rc = search_locked(x, &q, &r, false);
+    x->prof = prof;
+    e = hipStreamSynchronize(x->stream);
+  }
+  ids.release();
+  keys.release();
+  if (e != hipSuccess) return fail(BB_E_HIP, std::string("rank-0 table: ") + hipGetErrorString(e));
+  if (rc) return rc;
+  x->r0_ready = true;
+  return BB_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t in_dtype, int32_t prenormalized,
                     int32_t where, const uint32_t* present_bits) {
   BB_CHECK_INDEX(x, "bb_upload_items");
@@ -641,6 +719,8 @@ int bb_upload_items(bb_index* x, const void* rows, int64_t n, int32_t d, int32_t
   if ((rc = upload_rows(x, rows, n, d, in_dtype, prenormalized ? 0 : 1, where, x->items.p, x->Dpad))) return rc;
   if ((rc = make_planes(x, x->items, x->items3, x->Dpad))) return rc;
   if ((rc = make_rr(x, x->items, x->items_bf, x->Dpad, x->Dpad_b, 0))) return rc;
+  x->r0_ready = false;
+  if (x->dtype == F32 && x->items_bf.p && n <= (int64_t)kCompactMaxWords * 32 && (rc = build_r0(x))) return rc;
   return scope.leave();
 }
 
@@ -749,6 +829,138 @@ int bb_key_lens(const bb_query* q, int32_t* sides, int32_t* k_int) { return side
 namespace {
 
 constexpr int kRetrySlab = 1;  // search_locked: a streaming candidate region overflowed
+constexpr int kNoCompact = 2;  // search_locked of a shadow: its shapes leave the list path (nothing launched)
+
+// Constraint-first search (compact.hip, the reference's "apply hard constraints first",
+// recommendation_system.py:628-656): the `cnt` rows mask d_mask allows are packed into the
+// shadow index x->cx (positions in ascending id order, so ties still break by id), with the
+// liked sets' rows, their rank-0 exclusions and the per-query exclusions re-indexed, in ONE
+// launch; the unchanged search then runs over the packed rows and writes idmap[position] as
+// each id.  Returns kNoCompact (having launched only the packing kernel) when the shadow's
+// shapes would leave the list path, whose writers map the ids.
+int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s, const void* d_rows,
+                   const void* d_items, const void* d_cf, const void* d_mask, const void* d_excl, int64_t cnt) {
+  const bool need_content = q->mode != BB_MODE_CF;
+  const bool need_cf = q->mode == BB_MODE_CF || q->mode == BB_MODE_HYBRID;
+  const bool liked = need_content && q->mode != BB_MODE_SEMANTIC;
+  const int B = q->B;
+  bb_index* c = x->cx;
+  if (!c) {
+    c = new bb_index();
+    c->magic = 0;  // never a caller's handle
+    c->shadow = true;
+    c->device = x->device;
+    c->dtype = F32;
+    x->cx = c;
+  }
+  c->lists_opt = x->lists_opt;
+  c->sq_opt = 0;       // the packed search is the list path (B > kSqMaxB anyway)
+  c->stream_opt = 0;
+  c->refine_opt = 0;
+  c->ws_cap = x->ws_cap;
+  c->ws_set = x->ws_set;
+  c->prof = x->prof;
+  const int64_t cap = round_up(std::max<int64_t>(cnt, 1), kTileRows);
+  const int cnw = (int)(cap / 32);
+  c->n = std::max<int64_t>(cnt, 1);  // (no allowed item: one padding row, never present)
+  c->Npad = cap;
+  c->d = x->d;
+  c->Dpad = x->Dpad;
+  c->Dpad_b = x->Dpad_b;
+  c->r = x->r;
+  c->Rpad = x->Rpad;
+  c->Rpad_b = x->Rpad_b;
+  c->id_offset = 0;
+  c->rr_stats.p = x->rr_stats.p;  // bounds over every row hold for any subset of them
+  c->rr_stats.cap = x->rr_stats.cap;
+  c->rr_stats.owned = false;
+  int rc;
+  const size_t wb = (size_t)cnw * 4;
+  if ((rc = c->ones.ensure(wb)) || (rc = c->zeros.ensure(wb)) || (rc = c->idmap.ensure((size_t)cap * 4))) return rc;
+  if (c->filled_words < (size_t)cnw) {  // constant fills, once per size (outside any plan record)
+    BB_HIP(hipMemsetAsync(c->ones.p, 0xFF, c->ones.cap, s));
+    BB_HIP(hipMemsetAsync(c->zeros.p, 0, c->zeros.cap, s));
+    c->filled_words = c->ones.cap / 4;
+  }
+  if (need_content &&
+      ((rc = c->items.ensure((size_t)cap * x->Dpad * 4)) || (rc = c->items_bf.ensure((size_t)cap * x->Dpad_b * 2)) ||
+       (rc = c->items_present.ensure(wb))))
+    return rc;
+  if (need_cf && ((rc = c->cf.ensure((size_t)cap * x->Rpad * 4)) || (rc = c->cf_bf.ensure((size_t)cap * x->Rpad_b * 2)) ||
+                  (rc = c->cf_present.ensure(wb))))
+    return rc;
+  if (liked && ((rc = c->cq_rows.ensure((size_t)B * x->d * 4)) || (rc = c->cexcl0.ensure((size_t)B * wb)))) return rc;
+  if (need_cf && d_excl && (rc = c->cexcl1.ensure((size_t)B * wb))) return rc;
+  CompactArgs a{};
+  a.mask = (const uint32_t*)d_mask;
+  a.n = x->n;
+  a.nw = (int32_t)((x->n + 31) / 32);
+  a.id_offset = (uint32_t)x->id_offset;
+  if (need_content) {
+    a.items = (const float*)x->items.p;
+    a.ld = x->Dpad;
+    a.items_bf = (const uint16_t*)x->items_bf.p;
+    a.ld_b = x->Dpad_b;
+    a.items_present = (const uint32_t*)x->items_present.p;
+    a.c_items = (float*)c->items.p;
+    a.c_items_bf = (uint16_t*)c->items_bf.p;
+    a.c_present = (uint32_t*)c->items_present.p;
+  }
+  if (need_cf) {
+    a.cf = (const float*)x->cf.p;
+    a.ldc = x->Rpad;
+    a.cf_bf = (const uint16_t*)x->cf_bf.p;
+    a.ldc_b = x->Rpad_b;
+    a.cf_present = (const uint32_t*)x->cf_present.p;
+    a.c_cf = (float*)c->cf.p;
+    a.c_cf_bf = (uint16_t*)c->cf_bf.p;
+    a.c_cf_present = (uint32_t*)c->cf_present.p;
+  }
+  a.cap = (int32_t)cap;
+  a.cnw = cnw;
+  a.n_pos_wg = (int32_t)(cap / 64);
+  a.idmap = (uint32_t*)c->idmap.p;
+  const bool per_query = liked || (need_cf && d_excl);
+  a.B = per_query ? B : 0;
+  if (liked) {
+    a.q_items = (const int64_t*)d_items;
+    a.q_rows = (float*)c->cq_rows.p;
+    a.d = x->d;
+    a.r0key = (const uint64_t*)x->r0key.p;
+    a.c_excl0 = (uint32_t*)c->cexcl0.p;
+  }
+  if (need_cf && d_excl) {
+    a.excl = (const uint32_t*)d_excl;
+    a.excl_ld = a.nw;
+    a.c_excl1 = (uint32_t*)c->cexcl1.p;
+  }
+  if ((rc = timed(x, K_PREP, s, [&] { return launch_compact(a, s); }))) return rc;
+  bb_query q2 = *q;
+  q2.where = BB_DEVICE;
+  q2.stream = s;
+  q2.flags = (q->flags & ~BB_Q_NULL_STREAM) | (s ? 0 : BB_Q_NULL_STREAM);
+  q2.mask_bits = nullptr;
+  q2.mask_count = 0;
+  q2.excl_bits = need_cf && d_excl ? (const uint32_t*)c->cexcl1.p : nullptr;
+  if (liked) {
+    q2.q_items = nullptr;
+    q2.q_rows = c->cq_rows.p;
+    q2.q_dtype = F32;
+  } else {
+    q2.q_rows = d_rows;
+  }
+  q2.q_cf = d_cf;
+  c->cur_cexcl = liked ? (const uint32_t*)c->cexcl0.p : nullptr;
+  rc = search_locked(c, &q2, res, false);
+  // the shadow's kernels count as this handle's
+  for (auto& pe : c->pending) x->pending.push_back(pe);
+  c->pending.clear();
+  for (int i = 0; i < K_NFAM; ++i) {
+    x->launches[i] += c->launches[i];
+    c->launches[i] = 0;
+  }
+  return rc;
+}
 
 int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_stream) {
   int32_t sides, K_int;
@@ -759,7 +971,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
   if (x->n <= 0) return fail(BB_E_STATE, "no items uploaded");
   const bool need_content = q->mode != BB_MODE_CF;
   const bool need_cf = q->mode == BB_MODE_CF || q->mode == BB_MODE_HYBRID;
-  const bool drop = q->mode == BB_MODE_SIMILAR || q->mode == BB_MODE_HYBRID;
+  // (a shadow's packed rows drop the rank-0 item through its content exclusions instead)
+  const bool drop = (q->mode == BB_MODE_SIMILAR || q->mode == BB_MODE_HYBRID) && !x->shadow;
   if (need_cf && !x->cf.p) return fail(BB_E_STATE, "CF mode needs bb_upload_cf");
   if (need_content && q->mode != BB_MODE_SEMANTIC && !q->q_items && !q->q_rows)
     return fail(BB_E_ARG, "similar/hybrid mode needs q_items (or pre-normalised q_rows)");
@@ -862,6 +1075,31 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       (rc = to_device(x, x->stage_in, off_mask, q->mask_bits, b_mask, where, s, &d_mask)) ||
       (rc = to_device(x, x->stage_in, off_excl, q->excl_bits, b_excl, where, s, &d_excl)))
     return rc;
+
+  // ---- constraint-first search: a selective mask with a known count (host masks are counted
+  // here; device masks carry bb_query.mask_count) on a one-slab f32 index packs its allowed
+  // rows and searches only them (compact_search).  BB_OPT_PREFILTER: -1 auto (allowed rows
+  // <= n/4), 0 off, 1 whenever the count is known. ----
+  if (!x->shadow && d_mask && !out_keys && B > kSqMaxB && x->prefilter_opt != 0 && x->dtype == F32 &&
+      x->n <= (int64_t)kCompactMaxWords * 32 && x->lists_opt != 0 && x->stream_opt != 1 &&
+      (!need_content || (x->items_bf.p && x->Dpad <= kRrMaxD && x->d <= kRrMaxD)) && (!need_cf || x->cf_bf.p) &&
+      (q->mode == BB_MODE_SEMANTIC || q->mode == BB_MODE_CF || (d_items && x->r0_ready))) {
+    int64_t cnt = -1;
+    if (where == BB_HOST) {
+      cnt = 0;
+      for (int64_t w = 0; w < nw; ++w) {
+        uint32_t v = q->mask_bits[w];
+        if ((w + 1) * 32 > x->n) v &= (1u << (x->n & 31)) - 1u;
+        cnt += __builtin_popcount(v);
+      }
+    } else if (q->mask_count > 0) {
+      cnt = std::min<int64_t>(q->mask_count, x->n);
+    }
+    if (cnt >= 0 && (x->prefilter_opt == 1 || cnt * 4 <= x->n)) {
+      rc = compact_search(x, q, res, s, d_rows, d_items, d_cf, d_mask, d_excl, cnt);
+      if (rc != kNoCompact) return rc;
+    }
+  }
 
   // ---- small batches (the reference's request shape: one target row, one user, one
   // retriever query, one HybridRecommender request): one approximate pass over the bf16 copy
@@ -1192,6 +1430,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         ((rc = x->lists.ensure(list_b[0] + list_b[1])) ||
          (list_c && drop && (rc = x->r0lists.ensure((size_t)l_nch[0] * (bpad / 32) * 64 * 8)))))
       return rc;
+    // a shadow's ids are mapped by the list select / finalize1 writers only: any other path
+    // leaves it before its first launch (the caller then runs the full search)
+    if (x->shadow && ((need_content && !list_c) || (need_cf && !list_f)))
+      return b0 == 0 ? kNoCompact : fail(BB_E_STATE, "internal: a packed search's later query chunk left the list path");
     // the prep launches of both sides (hybrid) go out as one launch
     const bool prep_c = need_content && !fuse_c && !rrfuse_c && !rraw_c, prep_f = need_cf && !fuse_f && !rrfuse_f;
     PrepArgs pa_c{}, pa_f{};
@@ -1314,10 +1556,13 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         ga.n_valid = ncols;
         ga.slab_start = c0;
         // the scan epilogue is branch-free: every bitset pointer is valid
-        const bool has_excl = cf_side && d_excl;
+        // per-query exclusions: the CF side's rated items; in a shadow also the content side's
+        // rank-0 item (x->cur_cexcl)
+        const uint32_t* side_excl = cf_side ? (const uint32_t*)d_excl : x->cur_cexcl;
+        const bool has_excl = side_excl != nullptr;
         ga.mask = d_mask ? (const uint32_t*)d_mask : (const uint32_t*)x->ones.p;
         ga.present = (const uint32_t*)(cf_side ? x->cf_present.p : x->items_present.p);
-        ga.excl = has_excl ? (const uint32_t*)d_excl + (size_t)b0 * nw : (const uint32_t*)x->zeros.p;
+        ga.excl = has_excl ? side_excl + (size_t)b0 * nw : (const uint32_t*)x->zeros.p;
         ga.excl_ld = has_excl ? nw : 0;
         ga.tmax = (uint32_t*)x->tmax.p + (dual && side ? (size_t)Bc * ldt * 2 : 0);
         // present maxima only where a rank 0 is dropped (the content side of similar / hybrid):
@@ -1520,7 +1765,8 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         sa.gid0 = (uint32_t)(x->id_offset + c0);
         sa.mask = (const uint32_t*)d_mask;
         sa.present = (const uint32_t*)(cf_side ? x->cf_present.p : x->items_present.p);
-        sa.excl = cf_side && d_excl ? (const uint32_t*)d_excl + (size_t)b0 * nw : nullptr;
+        sa.excl = has_excl ? side_excl + (size_t)b0 * nw : nullptr;
+        sa.idmap = x->shadow ? (const uint32_t*)x->idmap.p : nullptr;
         sa.excl_ld = nw;
         sa.K = K_int;
         // blocked score image: the split scan, and the bf16 scan with 64 queries per wave
@@ -1748,6 +1994,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     fa.ids = o_id + (size_t)b0 * q->k;
     fa.counts = o_cnt ? o_cnt + b0 : nullptr;
     fa.n_rows = bc;
+    fa.idmap = x->shadow ? (const uint32_t*)x->idmap.p : nullptr;
     static const bool fin_trace = kProbes && ab_env("BB_SELECT_TRACE") != nullptr;
     if (fin_trace) {
       if ((rc = x->trace.ensure((size_t)bc * 8 * 8))) return rc;
@@ -1919,6 +2166,10 @@ int bb_set_option(bb_index* x, int32_t option, int64_t value) {
       if (value < -1 || value > 1) return fail(BB_E_ARG, "BB_OPT_SMALL_BATCH must be -1, 0 or 1");
       x->sq_opt = (int)value;
       return BB_OK;
+    case BB_OPT_PREFILTER:
+      if (value < -1 || value > 1) return fail(BB_E_ARG, "BB_OPT_PREFILTER must be -1, 0 or 1");
+      x->prefilter_opt = (int)value;
+      return BB_OK;
     case BB_OPT_WORKSPACE_BYTES:
       if (value < (1ll << 20)) return fail(BB_E_ARG, "BB_OPT_WORKSPACE_BYTES must be >= 1 MiB");
       x->ws_cap = value;
@@ -2003,6 +2254,7 @@ int bb_plan_create(bb_index* x, const bb_query* q, const bb_result* res, bb_plan
     v->refine_opt = x->refine_opt;
     v->lists_opt = x->lists_opt;
     v->sq_opt = x->sq_opt;
+    v->prefilter_opt = x->prefilter_opt;
     v->ws_cap = x->ws_cap;
     v->ws_set = x->ws_set;
   }
@@ -2025,7 +2277,10 @@ int bb_plan_create(bb_index* x, const bb_query* q, const bb_result* res, bb_plan
     g_err = msg;
     return rc == kRetrySlab ? BB_E_HOSTSYNC : rc;
   }
-  if (hipEventCreateWithFlags(&p->done, hipEventDisableTiming) != hipSuccess) {
+  // completion only (destroy frees the view after it): no system-scope release fence — with
+  // the default flags each replay's event wrote back and invalidated the caches, +5 us on a
+  // one-query plan (r06b plan_latency: similar_k10 19.6 -> 24.5 us)
+  if (hipEventCreateWithFlags(&p->done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
     delete p;
     (void)bb_destroy(v);
     return fail(BB_E_HIP, "bb_plan_create: hipEventCreateWithFlags failed");

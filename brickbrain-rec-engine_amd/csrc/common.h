@@ -375,6 +375,9 @@ struct SelectArgs {
   const float* rr_q_raw;
   int64_t rr_q_raw_ld;
   int32_t rr_q_raw_d;       // real row width (elements past it are zero, as prep's)
+  // constraint-first search (compact.hip): keys carry positions in the packed rows; the final
+  // ids written are idmap[position] (global ids), null = keys carry global ids
+  const uint32_t* idmap;
 };
 constexpr int kRrCap = 512;
 constexpr int kRrR0Cap = 64;
@@ -415,7 +418,51 @@ struct FinalizeArgs {
   int64_t* ids;             // [B][k]
   int32_t* counts;          // [B] or null
   uint64_t* trace;          // probe runs (BB_SELECT_TRACE): per-row phase stamps, or null
+  const uint32_t* idmap;    // packed-row positions -> global ids (SelectArgs.idmap), or null
 };
+__device__ __forceinline__ int64_t out_id(const uint32_t* idmap, uint32_t g) {
+  return idmap ? (int64_t)idmap[g] : (int64_t)g;
+}
+
+// Constraint-first search (compact.hip): the rows a mask allows, packed.  Positions [0, cap)
+// of the packed buffers; position p holds the p-th allowed item (ascending ids).
+constexpr int kCompactMaxWords = 2048;  // mask words: indexes of up to 65,536 rows
+struct CompactArgs {
+  const uint32_t* mask;      // [nw] allowed items (device)
+  int64_t n;                 // items of the index
+  int32_t nw;                // ceil(n / 32)
+  uint32_t id_offset;        // global id of local row 0
+  const float* items;        // f32 content rows [Npad][ld], or null (no content side)
+  int64_t ld;
+  const uint16_t* items_bf;  // their f16 copy [Npad][ld_b]
+  int64_t ld_b;
+  const uint32_t* items_present;
+  const float* cf;           // f32 CF rows [Npad][ldc], or null (no CF side)
+  int64_t ldc;
+  const uint16_t* cf_bf;
+  int64_t ldc_b;
+  const uint32_t* cf_present;
+  int32_t cap;               // packed rows (multiple of 64; >= the allowed count)
+  int32_t cnw;               // cap / 32
+  int32_t n_pos_wg;          // cap / 64 position workgroups
+  uint32_t* idmap;           // [cap] global id per position (0xFFFFFFFF: padding)
+  float* c_items;
+  uint16_t* c_items_bf;
+  uint32_t* c_present;       // [cnw]
+  float* c_cf;
+  uint16_t* c_cf_bf;
+  uint32_t* c_cf_present;
+  int32_t B;                 // query workgroups
+  const int64_t* q_items;    // [B] liked sets (global ids), with q_rows
+  float* q_rows;             // [B][d] their stored f32 rows out, or null
+  int32_t d;
+  const uint64_t* r0key;     // [n + 1] rank-0 key of each item's own row (the unmasked arg-max); [n]: a zero row's
+  uint32_t* c_excl0;         // [B][cnw] content exclusion: the rank-0 item's position, or null
+  const uint32_t* excl;      // [B][excl_ld] per-query exclusions over local rows, or null
+  int64_t excl_ld;
+  uint32_t* c_excl1;         // [B][cnw] the same re-indexed to positions, or null
+};
+hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 
 struct PrepArgs {
   const void* src;          // query rows [B][d] (q_dtype) or null

@@ -1,0 +1,188 @@
+// compact.hip — constraint-first search: the allowed rows of a selective mask gathered into a
+// compact shadow index, so the scans and the list select touch only them.
+//
+// The reference applies the hard constraints FIRST and scores inside the valid set:
+// HybridRecommender.get_recommendations step 1 (recommendation_system.py:628-640) turns the
+// constraints into valid_set_nums, then both sides walk only those sets (:648-656, the filter
+// walks at :229 and :454).  With the mask's count known on the host (the length of
+// valid_set_nums), bb_search does the same on the device: this kernel packs the allowed rows
+// — position p = the p-th allowed item, ascending, so (score desc, position asc) is exactly
+// (score desc, id asc) — and the per-query bits that refer to them, and the unchanged search
+// pipeline runs over the packed rows.  Scores are computed from bit-identical operands, so the
+// results are identical to the full scan's.
+//
+// One launch, two kinds of workgroup (every one first builds the popcount prefix of the mask
+// words in LDS — ≤ 2,048 words, L2-resident — so no workgroup waits for another):
+//   position workgroups  64 positions each: idmap, the f32 + f16 content rows, the f32 + f16
+//                        CF rows, the present bits of both item spaces (zero rows / bits for
+//                        the padding positions past the count)
+//   query workgroups     one per query row: the liked set's stored row (the content query of
+//                        similar / hybrid searches), the content exclusion of its rank-0 item
+//                        (the arg-max of the UNMASKED ranking, :217 — known per item from the
+//                        rank-0 table, so the packed search drops it as the full one does),
+//                        and the query's CF exclusions (rated items, :441-451) re-indexed to
+//                        positions
+#include "common.h"
+
+namespace bb {
+
+constexpr int kCompactThreads = 256;
+constexpr int kCompactPosPerWg = 64;
+
+// p-th set bit of w (0-based; p < popcount(w))
+__device__ __forceinline__ int select_bit(uint32_t w, int p) {
+  for (int i = 0; i < p; ++i) w &= w - 1u;
+  return __builtin_ctz(w);
+}
+
+__global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a) {
+  __shared__ uint32_t mw[kCompactMaxWords];
+  __shared__ uint32_t pre[kCompactMaxWords + 1];
+  __shared__ uint32_t rowbits[kCompactMaxWords];
+  __shared__ uint32_t scan[kCompactThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nw = a.nw;
+  // ---- mask words (bits past n cleared) and their exclusive popcount prefix ----
+  constexpr int kWpt = kCompactMaxWords / kCompactThreads;
+  uint32_t cnt[kWpt];
+  uint32_t mine = 0;
+#pragma unroll
+  for (int j = 0; j < kWpt; ++j) {
+    const int w = tid * kWpt + j;
+    uint32_t v = 0;
+    if (w < nw) {
+      v = a.mask[w];
+      if ((int64_t)(w + 1) * 32 > a.n) v &= (1u << (a.n & 31)) - 1u;
+      mw[w] = v;
+    }
+    cnt[j] = (uint32_t)__popc(v);
+    mine += cnt[j];
+  }
+  // block exclusive scan of the per-thread sums
+  uint32_t incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) scan[wave] = incl;
+  __syncthreads();
+  uint32_t base = incl - mine;
+  for (int w = 0; w < wave; ++w) base += scan[w];
+  const uint32_t total = scan[0] + scan[1] + scan[2] + scan[3];
+#pragma unroll
+  for (int j = 0; j < kWpt; ++j) {
+    const int w = tid * kWpt + j;
+    if (w < nw) pre[w] = base;
+    base += cnt[j];
+  }
+  if (tid == 0) pre[nw] = total;
+  __syncthreads();
+  // more allowed items than the caller's count: the packed search would miss items, so it
+  // finds none (every present bit 0 -> empty results) instead of a silently wrong list
+  const uint32_t E = total <= (uint32_t)a.cap ? total : 0u;
+
+  if ((int)blockIdx.x < a.n_pos_wg) {
+    // ---- positions [p0, p0 + 64): one wave per position in turn ----
+    const int p0 = blockIdx.x * kCompactPosPerWg;
+    if (tid < 2) rowbits[tid] = 0u, rowbits[2 + tid] = 0u;  // present words (content, CF) of this range
+    __syncthreads();
+    for (int pi = wave; pi < kCompactPosPerWg; pi += kCompactThreads / 64) {
+      const int p = p0 + pi;
+      int64_t item = -1;
+      if ((uint32_t)p < E) {  // the p-th allowed item: binary search over the prefix, then in-word
+        int lo = 0, hi = nw;  // pre[lo] <= p < pre[hi]
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (pre[mid] <= (uint32_t)p) lo = mid;
+          else hi = mid;
+        }
+        item = (int64_t)lo * 32 + select_bit(mw[lo], p - (int)pre[lo]);
+      }
+      if (lane == 0) a.idmap[p] = item >= 0 ? (uint32_t)(item + a.id_offset) : 0xFFFFFFFFu;
+      if (a.items) {
+        const float4* src = (const float4*)(a.items + (item >= 0 ? item : 0) * a.ld);
+        float4* dst = (float4*)(a.c_items + (int64_t)p * a.ld);
+        for (int c = lane; c < a.ld / 4; c += 64) dst[c] = item >= 0 ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const uint4* sb = (const uint4*)(a.items_bf + (item >= 0 ? item : 0) * a.ld_b);
+        uint4* db = (uint4*)(a.c_items_bf + (int64_t)p * a.ld_b);
+        for (int c = lane; c < a.ld_b / 8; c += 64) db[c] = item >= 0 ? sb[c] : make_uint4(0u, 0u, 0u, 0u);
+        if (lane == 0 && item >= 0 && ((a.items_present[item >> 5] >> (item & 31)) & 1u))
+          atomicOr(&rowbits[pi >> 5], 1u << (pi & 31));
+      }
+      if (a.cf) {
+        const float4* src = (const float4*)(a.cf + (item >= 0 ? item : 0) * a.ldc);
+        float4* dst = (float4*)(a.c_cf + (int64_t)p * a.ldc);
+        for (int c = lane; c < a.ldc / 4; c += 64) dst[c] = item >= 0 ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const uint4* sb = (const uint4*)(a.cf_bf + (item >= 0 ? item : 0) * a.ldc_b);
+        uint4* db = (uint4*)(a.c_cf_bf + (int64_t)p * a.ldc_b);
+        for (int c = lane; c < a.ldc_b / 8; c += 64) db[c] = item >= 0 ? sb[c] : make_uint4(0u, 0u, 0u, 0u);
+        if (lane == 0 && item >= 0 && ((a.cf_present[item >> 5] >> (item & 31)) & 1u))
+          atomicOr(&rowbits[2 + (pi >> 5)], 1u << (pi & 31));
+      }
+    }
+    __syncthreads();
+    if (tid < 2) {
+      if (a.items) a.c_present[(p0 >> 5) + tid] = rowbits[tid];
+      if (a.cf) a.c_cf_present[(p0 >> 5) + tid] = rowbits[2 + tid];
+    }
+    return;
+  }
+
+  // ---- query row b ----
+  const int b = blockIdx.x - a.n_pos_wg;
+  if (a.q_rows) {  // the liked set's stored row (zero for an id outside the index, as prep's gather)
+    const int64_t lid = a.q_items[b] - (int64_t)a.id_offset;
+    const bool ok = lid >= 0 && lid < a.n;
+    float* dst = a.q_rows + (int64_t)b * a.d;
+    const float* src = a.items + (ok ? lid : 0) * a.ld;
+    for (int c = tid; c < a.d; c += kCompactThreads) dst[c] = ok ? src[c] : 0.f;
+    if (a.c_excl0) {  // the rank-0 item, where it is allowed
+      for (int w = tid; w < a.cnw; w += kCompactThreads) rowbits[w] = 0u;
+      __syncthreads();
+      if (tid == 0) {
+        const uint64_t key = a.r0key[ok ? lid : a.n];  // [n]: a zero row's rank 0
+        const int64_t r = key ? (int64_t)gid_of(key) - (int64_t)a.id_offset : -1;
+        if (r >= 0 && r < a.n && ((mw[r >> 5] >> (r & 31)) & 1u)) {
+          const uint32_t p = pre[r >> 5] + (uint32_t)__popc(mw[r >> 5] & ((1u << (r & 31)) - 1u));
+          if (p < E) rowbits[p >> 5] |= 1u << (p & 31);
+        }
+      }
+      __syncthreads();
+      uint32_t* out = a.c_excl0 + (int64_t)b * a.cnw;
+      for (int w = tid; w < a.cnw; w += kCompactThreads) out[w] = rowbits[w];
+      __syncthreads();
+    }
+  }
+  if (a.c_excl1) {  // the query's exclusions, re-indexed to positions
+    for (int w = tid; w < a.cnw; w += kCompactThreads) rowbits[w] = 0u;
+    __syncthreads();
+    const uint32_t* ex = a.excl + (int64_t)b * a.excl_ld;
+    for (int w = tid; w < nw; w += kCompactThreads) {
+      uint32_t hit = mw[w] & ex[w];
+      while (hit) {
+        const int bit = __builtin_ctz(hit);
+        hit &= hit - 1u;
+        const uint32_t p = pre[w] + (uint32_t)__popc(mw[w] & ((1u << bit) - 1u));
+        if (p < E) atomicOr(&rowbits[p >> 5], 1u << (p & 31));
+      }
+    }
+    __syncthreads();
+    uint32_t* out = a.c_excl1 + (int64_t)b * a.cnw;
+    for (int w = tid; w < a.cnw; w += kCompactThreads) out[w] = rowbits[w];
+  }
+}
+
+hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
+  if (a.nw <= 0 || a.nw > kCompactMaxWords || a.cap <= 0 || a.cap % kCompactPosPerWg || a.cnw * 32 != a.cap ||
+      a.cnw > kCompactMaxWords || a.n_pos_wg * kCompactPosPerWg != a.cap || a.B < 0 ||
+      (a.items && (!a.items_bf || !a.c_items || !a.c_items_bf || !a.c_present || a.ld % 4 || a.ld_b % 8)) ||
+      (a.cf && (!a.cf_bf || !a.c_cf || !a.c_cf_bf || !a.c_cf_present || a.ldc % 4 || a.ldc_b % 8)) ||
+      (a.q_rows && (!a.q_items || !a.items || a.d <= 0 || a.d > a.ld)) || (a.c_excl0 && (!a.q_rows || !a.r0key)) ||
+      (a.c_excl1 && (!a.excl || a.excl_ld < a.nw)))
+    return hipErrorInvalidValue;
+  bb_launch(compact_kernel, dim3(a.n_pos_wg + a.B), dim3(kCompactThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace bb

@@ -11,6 +11,15 @@ namespace bb {
 
 constexpr int kFinThreads = 256;
 
+// h = wc·c + wcf·cf exactly as the reference's Python evaluates it (:812-818): two rounded
+// products, one rounded sum.  Without the pragma the compiler contracts it to fma(wc, c, wcf·cf),
+// which can differ in the last bit of h and so reorder near-tied blends (v_fma_f64 in the r05
+// finalize kernels).
+__device__ __forceinline__ double blend_h(double wc, double c, double wf, double f) {
+#pragma clang fp contract(off)
+  return wc * c + wf * f;
+}
+
 __device__ __forceinline__ uint64_t ord64_of(double d) {
   const uint64_t u = __builtin_bit_cast(uint64_t, d);
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
@@ -83,7 +92,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
       if (i < n) {
         const uint64_t key = lst[side][start[side] + i];
         sc[i] = float_of_ord(ordk_of(key));
-        id[i] = (int64_t)gid_of(key);
+        id[i] = out_id(a.idmap, gid_of(key));
       } else {
         sc[i] = 0.f;
         id[i] = -1;
@@ -129,7 +138,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
     if (hit >= 0) used[hit] = 1;
     const double cs = (double)float_of_ord(ordk_of(L0[i]));
     const double fs = hit >= 0 ? (double)float_of_ord(ordk_of(L1[hit])) : 0.0;
-    eh[i] = a.w_content * cs + a.w_cf * fs;
+    eh[i] = blend_h(a.w_content, cs, a.w_cf, fs);
     ek[i] = ord64_of(eh[i]);
     ehi[i] = ord_of((float)eh[i]);
     eg[i] = g;
@@ -140,7 +149,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
     const uint32_t g = gid_of(L1[j]);
     if (!used[j]) {
       const int pos = c[0] + atomicAdd(&n_ent, 1);
-      eh[pos] = a.w_content * 0.0 + a.w_cf * (double)float_of_ord(ordk_of(L1[j]));
+      eh[pos] = blend_h(a.w_content, 0.0, a.w_cf, (double)float_of_ord(ordk_of(L1[j])));
       ek[pos] = ord64_of(eh[pos]);
       ehi[pos] = ord_of((float)eh[pos]);
       eg[pos] = g;
@@ -193,7 +202,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
     }
     if (rank < a.k) {
       sc[rank] = (float)eh[e];
-      id[rank] = (int64_t)g;
+      id[rank] = out_id(a.idmap, g);
     }
   }
   for (int i = n + tid; i < a.k; i += kFinThreads) {

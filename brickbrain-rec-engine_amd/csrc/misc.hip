@@ -403,7 +403,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
     for (int i = tid; i < a.k; i += kFinThreads) {
       if (i < c) {
         sc[i] = float_of_ord(ordk_of(lists[side][i]));
-        id[i] = (int64_t)gid_of(lists[side][i]);
+        id[i] = out_id(a.idmap, gid_of(lists[side][i]));
       } else {
         sc[i] = 0.f;
         id[i] = -1;
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
         fs = (double)float_of_ord(ordk_of(lists[1][j]));
         break;
       }
-    const double h = a.w_content * cs + a.w_cf * fs;
+    const double h = blend_h(a.w_content, cs, a.w_cf, fs);
     const int pos = atomicAdd(&n_ent, 1);
     ent[pos] = Blend{ord64_of(h), g, 0u, h};
   }
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
         break;
       }
     if (in_c) continue;
-    const double h = a.w_content * 0.0 + a.w_cf * (double)float_of_ord(ordk_of(lists[1][j]));
+    const double h = blend_h(a.w_content, 0.0, a.w_cf, (double)float_of_ord(ordk_of(lists[1][j])));
     const int pos = atomicAdd(&n_ent, 1);
     ent[pos] = Blend{ord64_of(h), g, 0u, h};
   }
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
   for (int i = tid; i < a.k; i += kFinThreads) {
     if (i < c) {
       sc[i] = (float)ent[i].hv;
-      id[i] = (int64_t)ent[i].gid;
+      id[i] = out_id(a.idmap, ent[i].gid);
     } else {
       sc[i] = 0.f;
       id[i] = -1;

@@ -498,7 +498,7 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
           const int pos = (int)rk[e] - start;
           if (tid + e * kSelectThreads < Mc && pos >= 0 && pos < c) {
             sc[pos] = float_of_ord(ordk_of(mk[e]));
-            id[pos] = (int64_t)gid_of(mk[e]);
+            id[pos] = out_id(a.idmap, gid_of(mk[e]));
           }
         }
         for (int i = c + tid; i < a.k_final; i += kSelectThreads) {
@@ -579,7 +579,7 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     int64_t* id = a.out_ids + (size_t)row * a.k_final;
     for (int i = tid; i < a.k_final; i += kSelectThreads) {
       sc[i] = i < c ? float_of_ord(ordk_of(sel[start + i])) : 0.f;
-      id[i] = i < c ? (int64_t)gid_of(sel[start + i]) : (int64_t)-1;
+      id[i] = i < c ? out_id(a.idmap, gid_of(sel[start + i])) : (int64_t)-1;
     }
     if (a.out_counts && tid == 0) a.out_counts[row] = c;
     return;

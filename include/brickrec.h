@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 1
+#define BB_ABI_VERSION 2
 
 /* status codes */
 #define BB_OK 0
@@ -145,6 +145,12 @@ typedef struct {
                                   the user rated, :441-451); NULL = none              */
   double w_content, w_cf;      /* hybrid weights (0.4 / 0.6 at :609-610)               */
   void* stream;          /* hipStream_t to run on; NULL = the handle's stream          */
+  int64_t mask_count;    /* ABI 2: allowed items in mask_bits when the caller knows it (the
+                            length of the reference's valid_set_nums, :634), 0 = unknown.
+                            Host masks are counted by the library.  With a count the search
+                            may score only the allowed rows (BB_OPT_PREFILTER); a device
+                            mask_count must be >= the true count (if the device finds more
+                            allowed items than it, every result row comes back empty)      */
 } bb_query;
 
 typedef struct {
@@ -207,6 +213,15 @@ int bb_get_profile(bb_index* idx, bb_profile* out);
  *                           one approximate pass over the f16 copy per side and an exact
  *                           rescore of the candidates within its proven bound (no MFMA scan,
  *                           lists or list select) — the reference's one-query request shape.
+ *                           Results are identical either way.
+ *   BB_OPT_PREFILTER        -1 auto (default), 0 off, 1 whenever the mask's count is known:
+ *                           constraint-first search (the reference's step 1, "apply hard
+ *                           constraints first", recommendation_system.py:628-656).  The rows
+ *                           the mask allows are packed in one launch and only they are
+ *                           scanned, listed and rescored; auto = when at most n/4 rows are
+ *                           allowed, on f32 indexes of up to 65,536 rows, batches of more
+ *                           than 16 rows.  Similar / hybrid queries drop their rank-0 item
+ *                           (the unmasked arg-max) from a per-item table built at upload.
  *                           Results are identical either way. */
 #define BB_OPT_STREAM 1
 #define BB_OPT_STREAM_MIN_ITEMS 2
@@ -214,6 +229,7 @@ int bb_get_profile(bb_index* idx, bb_profile* out);
 #define BB_OPT_STREAM_REFINE 4
 #define BB_OPT_RR_LISTS 5
 #define BB_OPT_SMALL_BATCH 6
+#define BB_OPT_PREFILTER 7
 int bb_set_option(bb_index* idx, int32_t option, int64_t value);
 
 /* Stored (normalised, index-dtype) item rows of B global ids into out (B×d, row-major;

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in _declared() if not hasattr(lib, n)]
     assert not missing, missing
     assert set(_declared()) == set(L.EXPORTS)
-    assert lib.bb_abi_version() == 1
+    assert lib.bb_abi_version() == L.ABI_VERSION == 2
 
 
 def test_exports_are_c_linkage():
