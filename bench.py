@@ -451,8 +451,11 @@ def make_lane(brickrec, workload, base, B, local, dev, rank, j, inflight, extra)
         u = rng.normal(0.0, 0.1, (B, extra["f"].shape[1])).astype(np.float32)
         mw = torch.from_numpy(brickrec.bits_from_bool(mask).view(np.int32)).to(dev)
         ew = torch.from_numpy(brickrec.bits_from_bool(rated).view(np.int32)).to(dev)
+        # mask_count: the allowed rows' count (the reference's len(valid_set_nums), :634) lets
+        # the search pack them first (constraint-first, BB_OPT_PREFILTER) — computed here once
+        # per lane with the mask, as the serving path computes it with the constraint
         kw = dict(q_items=torch.from_numpy(liked).to(dev), q_cf=torch.from_numpy(u).to(dev), mask=mw, excl=ew,
-                  stream=s)
+                  stream=s, mask_count=int(np.count_nonzero(mask)))
         run, outs = idx.prepared_search("hybrid", TOPK, **kw)
         # the profiled runs go through bb_search on the lane's own handle (a plan replays on its
         # private view, which the lane's profiler does not see): the same kernels and arguments
@@ -636,6 +639,9 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="device-free rehearsal of the launcher and the reporting path (gloo ranks, no GPU)")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU-baseline timing")
+    ap.add_argument("--mall-flush", action="store_true",
+                    help="flush the 256 MiB Infinity Cache before every timed step (cold-MALL profiling runs; "
+                         "use with --inflight 1 under rocprofv3)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args)
@@ -699,13 +705,18 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    flush = torch.empty(640 << 20, dtype=torch.uint8, device=dev) if args.mall_flush else None
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if flush is not None:   # (profiling runs only: the fill is inside the window)
+            with torch.cuda.stream(lanes[i % len(lanes)][1]):
+                flush.fill_(i & 0xFF)
         lanes[i % len(lanes)][2]()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    del flush
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -756,6 +767,19 @@ def main():
     if args.dtype == "f32" and "gemm" in fam_us:
         # (hybrid: both sides, the CF factors padded to 64 f16 columns in the re-rank copy)
         roof["scan_reads"] = scan_read_roofline(B, DIM + (64 if hybrid else 0), fam_us["gemm"])
+    if hybrid:
+        # constraint-first search: the scans run over the rows the mask allows (packed), so the
+        # work they EXECUTE is 2·B·E·(d + r), E = allowed rows; `frac` above prices §8(d)'s
+        # full-index work (what the reference's CPU path does per query)
+        E = int(np.count_nonzero(q["mask"]))
+        ex_flops = 2.0 * B * E * (DIM + 50)
+        ex_bytes = E * (DIM + 50) * es + B * (50 * 4 + 8) + B * TOPK * 12
+        roof["prefilter"] = {
+            "allowed_rows": E, "of_rows": N_ITEMS,
+            "executed_flops": ex_flops, "executed_bytes": ex_bytes,
+            "executed_frac_of_step_mfma": round(ex_flops / (step_us * 1e-6) / 1e12 / BF16_DENSE_TF, 5),
+            "note": "the reference applies the hard constraints first (recommendation_system.py:628-656); "
+                    "bb_search packs the allowed rows (compact.hip, one launch) and scans / rescores only them"}
 
     # ---- MALL-cold latency (256 MiB Infinity Cache flushed before each step) ----
     flush = torch.empty(640 << 20, dtype=torch.uint8, device=dev)
@@ -769,7 +793,29 @@ def main():
         b.record(stream)
         torch.cuda.synchronize()
         cold.append(a.elapsed_time(b))
+    # the same kernels cold: the families' device times with the MALL
+    # flushed before every search, so the dominant kernel's frac is an HBM number, not a
+    # MALL one (the 39 MB index is Infinity-Cache-resident when warm)
+    idx.set_profiling(True)
+    n_cold = 20
+    for i in range(n_cold):
+        with torch.cuda.stream(stream):
+            flush.fill_((i + 7) & 0xFF)
+        run.prof_run()
+        torch.cuda.synchronize()
+    prof_c = idx.profile()
+    idx.set_profiling(False)
     del flush
+    fam_cold = {k: 1e3 * v["ms"] / n_cold for k, v in prof_c.items() if v["launches"] and k in fam_us}
+    dom = roof["family"]
+    rc_ = roofline(flops, alg_bytes, fam_cold[dom], args.dtype, roof["kernel"], mpf if dom == "gemm" else 1.0, None)
+    roof["cold"] = {"family": dom, "kernel_us": round(fam_cold[dom], 3), "bound": rc_["bound"],
+                    "achieved": rc_["achieved"], "unit": rc_["unit"], "frac": rc_["frac"],
+                    "hbm_gbs_at_alg_bytes": rc_["hbm_gbs_at_alg_bytes"],
+                    "hbm_frac_at_alg_bytes": rc_["hbm_frac_at_alg_bytes"],
+                    "kernels_us_per_step": {k: round(v, 3) for k, v in fam_cold.items()},
+                    "note": "the same search with the 256 MiB Infinity Cache flushed (640 MiB fill) before each step; "
+                            "warm numbers above are MALL-resident (the index is 39 MB)"}
 
     if hybrid:
         metric = "similarity queries/sec + p50 latency, hybrid content+CF + mask, 384-d x 25,216 items (configs[2])"
