@@ -918,6 +918,7 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
   }
   a.cap = (int32_t)cap;
   a.cnw = cnw;
+  a.xnw = (int32_t)((c->n + 31) / 32);  // the shadow search's exclusion row stride (its nw)
   a.n_pos_wg = (int32_t)(cap / 64);
   a.idmap = (uint32_t*)c->idmap.p;
   const bool per_query = liked || (need_cf && d_excl);

@@ -443,7 +443,8 @@ struct CompactArgs {
   int64_t ldc_b;
   const uint32_t* cf_present;
   int32_t cap;               // packed rows (multiple of 64; >= the allowed count)
-  int32_t cnw;               // cap / 32
+  int32_t cnw;               // cap / 32 (words of the packed present bitsets)
+  int32_t xnw;               // words per row of the packed exclusions (the shadow's ceil(count / 32))
   int32_t n_pos_wg;          // cap / 64 position workgroups
   uint32_t* idmap;           // [cap] global id per position (0xFFFFFFFF: padding)
   float* c_items;
@@ -457,10 +458,10 @@ struct CompactArgs {
   float* q_rows;             // [B][d] their stored f32 rows out, or null
   int32_t d;
   const uint64_t* r0key;     // [n + 1] rank-0 key of each item's own row (the unmasked arg-max); [n]: a zero row's
-  uint32_t* c_excl0;         // [B][cnw] content exclusion: the rank-0 item's position, or null
+  uint32_t* c_excl0;         // [B][xnw] content exclusion: the rank-0 item's position, or null
   const uint32_t* excl;      // [B][excl_ld] per-query exclusions over local rows, or null
   int64_t excl_ld;
-  uint32_t* c_excl1;         // [B][cnw] the same re-indexed to positions, or null
+  uint32_t* c_excl1;         // [B][xnw] the same re-indexed to positions, or null
 };
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
     const float* src = a.items + (ok ? lid : 0) * a.ld;
     for (int c = tid; c < a.d; c += kCompactThreads) dst[c] = ok ? src[c] : 0.f;
     if (a.c_excl0) {  // the rank-0 item, where it is allowed
-      for (int w = tid; w < a.cnw; w += kCompactThreads) rowbits[w] = 0u;
+      for (int w = tid; w < a.xnw; w += kCompactThreads) rowbits[w] = 0u;
       __syncthreads();
       if (tid == 0) {
         const uint64_t key = a.r0key[ok ? lid : a.n];  // [n]: a zero row's rank 0
@@ -149,13 +149,13 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
         }
       }
       __syncthreads();
-      uint32_t* out = a.c_excl0 + (int64_t)b * a.cnw;
-      for (int w = tid; w < a.cnw; w += kCompactThreads) out[w] = rowbits[w];
+      uint32_t* out = a.c_excl0 + (int64_t)b * a.xnw;
+      for (int w = tid; w < a.xnw; w += kCompactThreads) out[w] = rowbits[w];
       __syncthreads();
     }
   }
   if (a.c_excl1) {  // the query's exclusions, re-indexed to positions
-    for (int w = tid; w < a.cnw; w += kCompactThreads) rowbits[w] = 0u;
+    for (int w = tid; w < a.xnw; w += kCompactThreads) rowbits[w] = 0u;
     __syncthreads();
     const uint32_t* ex = a.excl + (int64_t)b * a.excl_ld;
     for (int w = tid; w < nw; w += kCompactThreads) {
@@ -168,14 +168,14 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
       }
     }
     __syncthreads();
-    uint32_t* out = a.c_excl1 + (int64_t)b * a.cnw;
-    for (int w = tid; w < a.cnw; w += kCompactThreads) out[w] = rowbits[w];
+    uint32_t* out = a.c_excl1 + (int64_t)b * a.xnw;
+    for (int w = tid; w < a.xnw; w += kCompactThreads) out[w] = rowbits[w];
   }
 }
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
   if (a.nw <= 0 || a.nw > kCompactMaxWords || a.cap <= 0 || a.cap % kCompactPosPerWg || a.cnw * 32 != a.cap ||
-      a.cnw > kCompactMaxWords || a.n_pos_wg * kCompactPosPerWg != a.cap || a.B < 0 ||
+      a.cnw > kCompactMaxWords || a.xnw <= 0 || a.xnw > a.cnw || a.n_pos_wg * kCompactPosPerWg != a.cap || a.B < 0 ||
       (a.items && (!a.items_bf || !a.c_items || !a.c_items_bf || !a.c_present || a.ld % 4 || a.ld_b % 8)) ||
       (a.cf && (!a.cf_bf || !a.c_cf || !a.c_cf_bf || !a.c_cf_present || a.ldc % 4 || a.ldc_b % 8)) ||
       (a.q_rows && (!a.q_items || !a.items || a.d <= 0 || a.d > a.ld)) || (a.c_excl0 && (!a.q_rows || !a.r0key)) ||
