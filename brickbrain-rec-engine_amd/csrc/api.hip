@@ -853,7 +853,14 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
     c->dtype = F32;
     x->cx = c;
   }
-  c->lists_opt = x->lists_opt;
+  // a few thousand packed rows: the int16 score image (1 MB at configs[2]) and the image
+  // selects rescore ~K + margin rows per query, where the per-lane lists of so few tiles
+  // overflow (a list sees 16 items a tile and ~1/4 of the packed rows are candidates at
+  // configs[2]) and rescore most rows.  BB_PF_LISTS (A/B runs): 1 keeps the lists.
+  static const int pf_lists = ab_env("BB_PF_LISTS") ? atoi(ab_env("BB_PF_LISTS")) : -1;
+  c->lists_opt = x->lists_opt == 0 || pf_lists == 0 || (pf_lists < 0 && round_up(std::max<int64_t>(cnt, 1), kTileRows) <= 4096)
+                     ? 0
+                     : x->lists_opt;
   c->sq_opt = 0;       // the packed search is the list path (B > kSqMaxB anyway)
   c->stream_opt = 0;
   c->refine_opt = 0;
@@ -919,7 +926,12 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
   a.cap = (int32_t)cap;
   a.cnw = cnw;
   a.xnw = (int32_t)((c->n + 31) / 32);  // the shadow search's exclusion row stride (its nw)
-  a.n_pos_wg = (int32_t)(cap / 64);
+  a.n_word_wg = cnw;
+  a.ch_items = need_content ? x->Dpad / 4 : 0;
+  a.ch_items_b = need_content ? x->Dpad_b / 8 : 0;
+  a.ch_cf = need_cf ? x->Rpad / 4 : 0;
+  a.ch_cf_b = need_cf ? x->Rpad_b / 8 : 0;
+  a.n_copy_wg = (int32_t)((cap * (a.ch_items + a.ch_items_b + a.ch_cf + a.ch_cf_b) + 255) / 256);
   a.idmap = (uint32_t*)c->idmap.p;
   const bool per_query = liked || (need_cf && d_excl);
   a.B = per_query ? B : 0;
@@ -1431,9 +1443,9 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         ((rc = x->lists.ensure(list_b[0] + list_b[1])) ||
          (list_c && drop && (rc = x->r0lists.ensure((size_t)l_nch[0] * (bpad / 32) * 64 * 8)))))
       return rc;
-    // a shadow's ids are mapped by the list select / finalize1 writers only: any other path
-    // leaves it before its first launch (the caller then runs the full search)
-    if (x->shadow && ((need_content && !list_c) || (need_cf && !list_f)))
+    // a shadow's ids are mapped by the list / int16-image selects and finalize1 only: any other
+    // path leaves it before its first launch (the caller then runs the full search)
+    if (x->shadow && ((need_content && !list_c && !s16_c) || (need_cf && !list_f && !s16_f)))
       return b0 == 0 ? kNoCompact : fail(BB_E_STATE, "internal: a packed search's later query chunk left the list path");
     // the prep launches of both sides (hybrid) go out as one launch
     const bool prep_c = need_content && !fuse_c && !rrfuse_c && !rraw_c, prep_f = need_cf && !fuse_f && !rrfuse_f;

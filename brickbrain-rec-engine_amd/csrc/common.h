@@ -442,10 +442,12 @@ struct CompactArgs {
   const uint16_t* cf_bf;
   int64_t ldc_b;
   const uint32_t* cf_present;
-  int32_t cap;               // packed rows (multiple of 64; >= the allowed count)
+  int32_t cap;               // packed rows (multiple of 32; >= the allowed count)
   int32_t cnw;               // cap / 32 (words of the packed present bitsets)
   int32_t xnw;               // words per row of the packed exclusions (the shadow's ceil(count / 32))
-  int32_t n_pos_wg;          // cap / 64 position workgroups
+  int32_t n_word_wg;         // cap / 32 workgroups: id map + present words
+  int32_t n_copy_wg;         // workgroups of the row copies (one 16-B piece per thread)
+  int32_t ch_items, ch_items_b, ch_cf, ch_cf_b;  // 16-B pieces per row of each copy (0: absent)
   uint32_t* idmap;           // [cap] global id per position (0xFFFFFFFF: padding)
   float* c_items;
   uint16_t* c_items_bf;

@@ -11,11 +11,14 @@
 // pipeline runs over the packed rows.  Scores are computed from bit-identical operands, so the
 // results are identical to the full scan's.
 //
-// One launch, two kinds of workgroup (every one first builds the popcount prefix of the mask
+// One launch, three kinds of workgroup (every one first builds the popcount prefix of the mask
 // words in LDS — ≤ 2,048 words, L2-resident — so no workgroup waits for another):
-//   position workgroups  64 positions each: idmap, the f32 + f16 content rows, the f32 + f16
-//                        CF rows, the present bits of both item spaces (zero rows / bits for
-//                        the padding positions past the count)
+//   word workgroups      32 positions each: the id map and the present words of both item
+//                        spaces
+//   copy workgroups      one 16-B piece per thread of the packed rows (f32 + f16 content, f32 +
+//                        f16 CF; zeros for the padding past the count): every load independent,
+//                        one memory round trip (64 positions per workgroup walked in turn took
+//                        ~44 us at configs[2], r06c)
 //   query workgroups     one per query row: the liked set's stored row (the content query of
 //                        similar / hybrid searches), the content exclusion of its rank-0 item
 //                        (the arg-max of the UNMASKED ranking, :217 — known per item from the
@@ -27,7 +30,6 @@
 namespace bb {
 
 constexpr int kCompactThreads = 256;
-constexpr int kCompactPosPerWg = 64;
 
 // p-th set bit of w (0-based; p < popcount(w))
 __device__ __forceinline__ int select_bit(uint32_t w, int p) {
@@ -82,55 +84,65 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
   // finds none (every present bit 0 -> empty results) instead of a silently wrong list
   const uint32_t E = total <= (uint32_t)a.cap ? total : 0u;
 
-  if ((int)blockIdx.x < a.n_pos_wg) {
-    // ---- positions [p0, p0 + 64): one wave per position in turn ----
-    const int p0 = blockIdx.x * kCompactPosPerWg;
-    if (tid < 2) rowbits[tid] = 0u, rowbits[2 + tid] = 0u;  // present words (content, CF) of this range
-    __syncthreads();
-    for (int pi = wave; pi < kCompactPosPerWg; pi += kCompactThreads / 64) {
-      const int p = p0 + pi;
-      int64_t item = -1;
-      if ((uint32_t)p < E) {  // the p-th allowed item: binary search over the prefix, then in-word
-        int lo = 0, hi = nw;  // pre[lo] <= p < pre[hi]
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (pre[mid] <= (uint32_t)p) lo = mid;
-          else hi = mid;
-        }
-        item = (int64_t)lo * 32 + select_bit(mw[lo], p - (int)pre[lo]);
-      }
-      if (lane == 0) a.idmap[p] = item >= 0 ? (uint32_t)(item + a.id_offset) : 0xFFFFFFFFu;
-      if (a.items) {
-        const float4* src = (const float4*)(a.items + (item >= 0 ? item : 0) * a.ld);
-        float4* dst = (float4*)(a.c_items + (int64_t)p * a.ld);
-        for (int c = lane; c < a.ld / 4; c += 64) dst[c] = item >= 0 ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const uint4* sb = (const uint4*)(a.items_bf + (item >= 0 ? item : 0) * a.ld_b);
-        uint4* db = (uint4*)(a.c_items_bf + (int64_t)p * a.ld_b);
-        for (int c = lane; c < a.ld_b / 8; c += 64) db[c] = item >= 0 ? sb[c] : make_uint4(0u, 0u, 0u, 0u);
-        if (lane == 0 && item >= 0 && ((a.items_present[item >> 5] >> (item & 31)) & 1u))
-          atomicOr(&rowbits[pi >> 5], 1u << (pi & 31));
-      }
-      if (a.cf) {
-        const float4* src = (const float4*)(a.cf + (item >= 0 ? item : 0) * a.ldc);
-        float4* dst = (float4*)(a.c_cf + (int64_t)p * a.ldc);
-        for (int c = lane; c < a.ldc / 4; c += 64) dst[c] = item >= 0 ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const uint4* sb = (const uint4*)(a.cf_bf + (item >= 0 ? item : 0) * a.ldc_b);
-        uint4* db = (uint4*)(a.c_cf_bf + (int64_t)p * a.ldc_b);
-        for (int c = lane; c < a.ldc_b / 8; c += 64) db[c] = item >= 0 ? sb[c] : make_uint4(0u, 0u, 0u, 0u);
-        if (lane == 0 && item >= 0 && ((a.cf_present[item >> 5] >> (item & 31)) & 1u))
-          atomicOr(&rowbits[2 + (pi >> 5)], 1u << (pi & 31));
-      }
+  // the p-th allowed item (p < E): binary search over the prefix, then the bit inside the word
+  auto item_of = [&](int p) -> int64_t {
+    if ((uint32_t)p >= E) return -1;
+    int lo = 0, hi = nw;  // pre[lo] <= p < pre[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (pre[mid] <= (uint32_t)p) lo = mid;
+      else hi = mid;
     }
-    __syncthreads();
-    if (tid < 2) {
-      if (a.items) a.c_present[(p0 >> 5) + tid] = rowbits[tid];
-      if (a.cf) a.c_cf_present[(p0 >> 5) + tid] = rowbits[2 + tid];
+    return (int64_t)lo * 32 + select_bit(mw[lo], p - (int)pre[lo]);
+  };
+
+  const int g = blockIdx.x;
+  if (g < a.n_word_wg) {
+    // ---- positions [32g, 32g + 32): the id map and one present word per item space ----
+    if (wave == 0) {
+      const int p = g * 32 + (lane & 31);
+      const int64_t item = item_of(p);
+      if (lane < 32) a.idmap[p] = item >= 0 ? (uint32_t)(item + a.id_offset) : 0xFFFFFFFFu;
+      const bool pc = a.items && item >= 0 && ((a.items_present[item >> 5] >> (item & 31)) & 1u);
+      const bool pf = a.cf && item >= 0 && ((a.cf_present[item >> 5] >> (item & 31)) & 1u);
+      const uint64_t bc = __ballot(pc && lane < 32), bf = __ballot(pf && lane < 32);
+      if (lane == 0 && a.items) a.c_present[g] = (uint32_t)bc;
+      if (lane == 0 && a.cf) a.c_cf_present[g] = (uint32_t)bf;
     }
+    return;
+  }
+  if (g < a.n_word_wg + a.n_copy_wg) {
+    // ---- rows: one 16-B piece per thread over [cap positions] x [the pieces of a row's f32
+    // content, f16 content, f32 CF and f16 CF copies] (zero pieces for the padding) ----
+    const int64_t i = (int64_t)(g - a.n_word_wg) * kCompactThreads + tid;
+    const int per = a.ch_items + a.ch_items_b + a.ch_cf + a.ch_cf_b;
+    const int p = (int)(i / per);
+    if (p >= a.cap) return;
+    int c = (int)(i - (int64_t)p * per);
+    const int64_t item = item_of(p);
+    const int64_t it = item >= 0 ? item : 0;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    uint4* dst;
+    if (c < a.ch_items) {
+      if (item >= 0) v = ((const uint4*)(a.items + it * a.ld))[c];
+      dst = (uint4*)(a.c_items + (int64_t)p * a.ld) + c;
+    } else if ((c -= a.ch_items) < a.ch_items_b) {
+      if (item >= 0) v = ((const uint4*)(a.items_bf + it * a.ld_b))[c];
+      dst = (uint4*)(a.c_items_bf + (int64_t)p * a.ld_b) + c;
+    } else if ((c -= a.ch_items_b) < a.ch_cf) {
+      if (item >= 0) v = ((const uint4*)(a.cf + it * a.ldc))[c];
+      dst = (uint4*)(a.c_cf + (int64_t)p * a.ldc) + c;
+    } else {
+      c -= a.ch_cf;
+      if (item >= 0) v = ((const uint4*)(a.cf_bf + it * a.ldc_b))[c];
+      dst = (uint4*)(a.c_cf_bf + (int64_t)p * a.ldc_b) + c;
+    }
+    *dst = v;
     return;
   }
 
   // ---- query row b ----
-  const int b = blockIdx.x - a.n_pos_wg;
+  const int b = g - a.n_word_wg - a.n_copy_wg;
   if (a.q_rows) {  // the liked set's stored row (zero for an id outside the index, as prep's gather)
     const int64_t lid = a.q_items[b] - (int64_t)a.id_offset;
     const bool ok = lid >= 0 && lid < a.n;
@@ -174,14 +186,20 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
 }
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
-  if (a.nw <= 0 || a.nw > kCompactMaxWords || a.cap <= 0 || a.cap % kCompactPosPerWg || a.cnw * 32 != a.cap ||
-      a.cnw > kCompactMaxWords || a.xnw <= 0 || a.xnw > a.cnw || a.n_pos_wg * kCompactPosPerWg != a.cap || a.B < 0 ||
-      (a.items && (!a.items_bf || !a.c_items || !a.c_items_bf || !a.c_present || a.ld % 4 || a.ld_b % 8)) ||
-      (a.cf && (!a.cf_bf || !a.c_cf || !a.c_cf_bf || !a.c_cf_present || a.ldc % 4 || a.ldc_b % 8)) ||
+  const int per = a.ch_items + a.ch_items_b + a.ch_cf + a.ch_cf_b;
+  if (a.nw <= 0 || a.nw > kCompactMaxWords || a.cap <= 0 || a.cap % 32 || a.cnw * 32 != a.cap ||
+      a.cnw > kCompactMaxWords || a.xnw <= 0 || a.xnw > a.cnw || a.n_word_wg != a.cnw || a.B < 0 || per <= 0 ||
+      (int64_t)a.n_copy_wg * kCompactThreads < (int64_t)a.cap * per ||
+      (a.items && (!a.items_bf || !a.c_items || !a.c_items_bf || !a.c_present || a.ld % 4 || a.ld_b % 8 ||
+                   a.ch_items != a.ld / 4 || a.ch_items_b != a.ld_b / 8)) ||
+      (!a.items && (a.ch_items || a.ch_items_b)) ||
+      (a.cf && (!a.cf_bf || !a.c_cf || !a.c_cf_bf || !a.c_cf_present || a.ldc % 4 || a.ldc_b % 8 ||
+                a.ch_cf != a.ldc / 4 || a.ch_cf_b != a.ldc_b / 8)) ||
+      (!a.cf && (a.ch_cf || a.ch_cf_b)) ||
       (a.q_rows && (!a.q_items || !a.items || a.d <= 0 || a.d > a.ld)) || (a.c_excl0 && (!a.q_rows || !a.r0key)) ||
       (a.c_excl1 && (!a.excl || a.excl_ld < a.nw)))
     return hipErrorInvalidValue;
-  bb_launch(compact_kernel, dim3(a.n_pos_wg + a.B), dim3(kCompactThreads), 0, s, a);
+  bb_launch(compact_kernel, dim3(a.n_word_wg + a.n_copy_wg + a.B), dim3(kCompactThreads), 0, s, a);
   return hipGetLastError();
 }
 

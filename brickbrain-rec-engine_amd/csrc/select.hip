@@ -96,7 +96,7 @@ __device__ __forceinline__ void rr_slow_path(const SelectArgs& a, int row, int n
     int64_t* id = a.out_ids + (size_t)row * a.k_final;
     for (int i = tid; i < a.k_final; i += kSelectThreads) {
       sc[i] = i < c ? float_of_ord(ordk_of(sel[start + i])) : 0.f;
-      id[i] = i < c ? (int64_t)gid_of(sel[start + i]) : (int64_t)-1;
+      id[i] = i < c ? out_id(a.idmap, gid_of(sel[start + i])) : (int64_t)-1;
     }
     if (a.out_counts && tid == 0) a.out_counts[row] = c;
     return;
@@ -552,7 +552,7 @@ __device__ __forceinline__ void select_body(const SelectArgs& a, int row) {
       if (i < c) {
         const uint64_t key = cand[start + i];
         sc[i] = float_of_ord(ordk_of(key));
-        id[i] = (int64_t)gid_of(key);
+        id[i] = out_id(a.idmap, gid_of(key));
       } else {
         sc[i] = 0.f;
         id[i] = -1;
@@ -793,7 +793,7 @@ __global__ __launch_bounds__(kSelectThreads) void cand_select_kernel(CandSelectA
         const int pos = rk[e] - start;
         if (tid + e * kSelectThreads < m && pos >= 0 && pos < c) {
           sc[pos] = float_of_ord(ordk_of(mk[e]));
-          id[pos] = (int64_t)gid_of(mk[e]);
+          id[pos] = out_id(sa.idmap, gid_of(mk[e]));
         }
       }
       for (int i = c + tid; i < sa.k_final; i += kSelectThreads) {

@@ -257,7 +257,7 @@ __device__ __forceinline__ void wave_sort_emit(const uint64_t* cand, int cnt, co
       const int i = s * 64 + lane - start;
       if (i >= 0 && i < a.k_final) {
         sc[i] = i < c ? float_of_ord(ordk_of(v[s])) : 0.f;
-        id[i] = i < c ? (int64_t)gid_of(v[s]) : (int64_t)-1;
+        id[i] = i < c ? out_id(a.idmap, gid_of(v[s])) : (int64_t)-1;
       }
     }
     for (int i = 64 * E - start + lane; i < a.k_final; i += 64) {
