@@ -853,23 +853,31 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
     c->dtype = F32;
     x->cx = c;
   }
-  // a few thousand packed rows: the int16 score image (1 MB at configs[2]) and the image
-  // selects rescore ~K + margin rows per query, where the per-lane lists of so few tiles
-  // overflow (a list sees 16 items a tile and ~1/4 of the packed rows are candidates at
-  // configs[2]) and rescore most rows.  BB_PF_LISTS (A/B runs): 1 keeps the lists.
+  // the list path (BB_PF_LISTS=0, A/B runs: the int16-image selects — one wave per query
+  // rescoring its candidates, 111 vs 48 us at configs[2], r06d)
   static const int pf_lists = ab_env("BB_PF_LISTS") ? atoi(ab_env("BB_PF_LISTS")) : -1;
-  c->lists_opt = x->lists_opt == 0 || pf_lists == 0 || (pf_lists < 0 && round_up(std::max<int64_t>(cnt, 1), kTileRows) <= 4096)
-                     ? 0
-                     : x->lists_opt;
+  c->lists_opt = pf_lists == 0 ? 0 : x->lists_opt;
   c->sq_opt = 0;       // the packed search is the list path (B > kSqMaxB anyway)
   c->stream_opt = 0;
   c->refine_opt = 0;
   c->ws_cap = x->ws_cap;
   c->ws_set = x->ws_set;
   c->prof = x->prof;
-  const int64_t cap = round_up(std::max<int64_t>(cnt, 1), kTileRows);
+  // slot stride: allowed item p sits in slot p·stride, so a lane half's top-5 list of one
+  // tile covers at most 16 / stride allowed items — stride 4 when the top-K_int is a large
+  // share of the allowed rows (no list can overflow), 2 or 1 as it shrinks (compact.hip)
+  int32_t sides_q = 0, K_int = 0;
+  int rc = side_k_int(q, &sides_q, &K_int);
+  if (rc) return rc;
+  const int64_t e1 = std::max<int64_t>(cnt, 1);  // (no allowed item: one padding slot, never present)
+  static const int pf_stride = ab_env("BB_PF_STRIDE") ? atoi(ab_env("BB_PF_STRIDE")) : 0;
+  const int stride = pf_stride == 1 || pf_stride == 2 || pf_stride == 4 ? pf_stride
+                     : (int64_t)K_int * 4 >= e1                     ? 4
+                     : (int64_t)K_int * 16 >= e1                    ? 2
+                                                                    : 1;
+  const int64_t cap = round_up(e1 * stride, kTileRows);
   const int cnw = (int)(cap / 32);
-  c->n = std::max<int64_t>(cnt, 1);  // (no allowed item: one padding row, never present)
+  c->n = e1 * stride;
   c->Npad = cap;
   c->d = x->d;
   c->Dpad = x->Dpad;
@@ -881,7 +889,6 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
   c->rr_stats.p = x->rr_stats.p;  // bounds over every row hold for any subset of them
   c->rr_stats.cap = x->rr_stats.cap;
   c->rr_stats.owned = false;
-  int rc;
   const size_t wb = (size_t)cnw * 4;
   if ((rc = c->ones.ensure(wb)) || (rc = c->zeros.ensure(wb)) || (rc = c->idmap.ensure((size_t)cap * 4))) return rc;
   if (c->filled_words < (size_t)cnw) {  // constant fills, once per size (outside any plan record)
@@ -924,6 +931,8 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
     a.c_cf_present = (uint32_t*)c->cf_present.p;
   }
   a.cap = (int32_t)cap;
+  a.stride = stride;
+  a.cap_pos = (int32_t)(cap / stride);
   a.cnw = cnw;
   a.xnw = (int32_t)((c->n + 31) / 32);  // the shadow search's exclusion row stride (its nw)
   a.n_word_wg = cnw;
@@ -931,7 +940,7 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
   a.ch_items_b = need_content ? x->Dpad_b / 8 : 0;
   a.ch_cf = need_cf ? x->Rpad / 4 : 0;
   a.ch_cf_b = need_cf ? x->Rpad_b / 8 : 0;
-  a.n_copy_wg = (int32_t)((cap * (a.ch_items + a.ch_items_b + a.ch_cf + a.ch_cf_b) + 255) / 256);
+  a.n_copy_wg = (int32_t)((a.cap_pos * (a.ch_items + a.ch_cf) + cap * (a.ch_items_b + a.ch_cf_b) + 255) / 256);
   a.idmap = (uint32_t*)c->idmap.p;
   const bool per_query = liked || (need_cf && d_excl);
   a.B = per_query ? B : 0;

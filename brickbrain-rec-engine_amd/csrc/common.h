@@ -442,7 +442,9 @@ struct CompactArgs {
   const uint16_t* cf_bf;
   int64_t ldc_b;
   const uint32_t* cf_present;
-  int32_t cap;               // packed rows (multiple of 32; >= the allowed count)
+  int32_t cap;               // packed slots (multiple of 32; >= stride x the allowed count)
+  int32_t stride;            // allowed item p sits in slot p·stride (the other slots: padding)
+  int32_t cap_pos;           // cap / stride
   int32_t cnw;               // cap / 32 (words of the packed present bitsets)
   int32_t xnw;               // words per row of the packed exclusions (the shadow's ceil(count / 32))
   int32_t n_word_wg;         // cap / 32 workgroups: id map + present words

@@ -16,9 +16,14 @@
 //   word workgroups      32 positions each: the id map and the present words of both item
 //                        spaces
 //   copy workgroups      one 16-B piece per thread of the packed rows (f32 + f16 content, f32 +
-//                        f16 CF; zeros for the padding past the count): every load independent,
-//                        one memory round trip (64 positions per workgroup walked in turn took
-//                        ~44 us at configs[2], r06c)
+//                        f16 CF; zeros for the padding): every load independent, one memory
+//                        round trip (64 positions per workgroup walked in turn took ~44 us at
+//                        configs[2], r06c)
+// Allowed item p sits in slot p·stride.  With stride 4 each lane half of a 32-row MFMA tile
+// (items {0-3, 8-11, 16-19, 24-27} or the other four groups) holds at most four allowed
+// items, so a per-lane top-5 list of one tile never overflows: when the top-K is a large
+// share of the allowed rows (configs[2]: 101 of ~440), dense packing overflowed most lists
+// and the list select rescored most rows (48 us, r06d).
 //   query workgroups     one per query row: the liked set's stored row (the content query of
 //                        similar / hybrid searches), the content exclusion of its rank-0 item
 //                        (the arg-max of the UNMASKED ranking, :217 — known per item from the
@@ -82,7 +87,8 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
   __syncthreads();
   // more allowed items than the caller's count: the packed search would miss items, so it
   // finds none (every present bit 0 -> empty results) instead of a silently wrong list
-  const uint32_t E = total <= (uint32_t)a.cap ? total : 0u;
+  const uint32_t E = total <= (uint32_t)a.cap_pos ? total : 0u;
+  const int S = a.stride;
 
   // the p-th allowed item (p < E): binary search over the prefix, then the bit inside the word
   auto item_of = [&](int p) -> int64_t {
@@ -98,11 +104,11 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
 
   const int g = blockIdx.x;
   if (g < a.n_word_wg) {
-    // ---- positions [32g, 32g + 32): the id map and one present word per item space ----
+    // ---- slots [32g, 32g + 32): the id map and one present word per item space ----
     if (wave == 0) {
-      const int p = g * 32 + (lane & 31);
-      const int64_t item = item_of(p);
-      if (lane < 32) a.idmap[p] = item >= 0 ? (uint32_t)(item + a.id_offset) : 0xFFFFFFFFu;
+      const int sl = g * 32 + (lane & 31);
+      const int64_t item = sl % S ? -1 : item_of(sl / S);
+      if (lane < 32) a.idmap[sl] = item >= 0 ? (uint32_t)(item + a.id_offset) : 0xFFFFFFFFu;
       const bool pc = a.items && item >= 0 && ((a.items_present[item >> 5] >> (item & 31)) & 1u);
       const bool pf = a.cf && item >= 0 && ((a.cf_present[item >> 5] >> (item & 31)) & 1u);
       const uint64_t bc = __ballot(pc && lane < 32), bf = __ballot(pf && lane < 32);
@@ -112,30 +118,41 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
     return;
   }
   if (g < a.n_word_wg + a.n_copy_wg) {
-    // ---- rows: one 16-B piece per thread over [cap positions] x [the pieces of a row's f32
-    // content, f16 content, f32 CF and f16 CF copies] (zero pieces for the padding) ----
+    // ---- rows: one 16-B piece per thread over [allowed positions] x [the f32 content and CF
+    // pieces of a row] then [every slot] x [the f16 pieces the scans read] (zeros for the
+    // padding slots; the f32 rows of padding slots are never read: nothing there is present)
     const int64_t i = (int64_t)(g - a.n_word_wg) * kCompactThreads + tid;
-    const int per = a.ch_items + a.ch_items_b + a.ch_cf + a.ch_cf_b;
-    const int p = (int)(i / per);
-    if (p >= a.cap) return;
-    int c = (int)(i - (int64_t)p * per);
-    const int64_t item = item_of(p);
-    const int64_t it = item >= 0 ? item : 0;
+    const int per32 = a.ch_items + a.ch_cf, per16 = a.ch_items_b + a.ch_cf_b;
+    const int64_t n32 = (int64_t)E * per32;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     uint4* dst;
-    if (c < a.ch_items) {
-      if (item >= 0) v = ((const uint4*)(a.items + it * a.ld))[c];
-      dst = (uint4*)(a.c_items + (int64_t)p * a.ld) + c;
-    } else if ((c -= a.ch_items) < a.ch_items_b) {
-      if (item >= 0) v = ((const uint4*)(a.items_bf + it * a.ld_b))[c];
-      dst = (uint4*)(a.c_items_bf + (int64_t)p * a.ld_b) + c;
-    } else if ((c -= a.ch_items_b) < a.ch_cf) {
-      if (item >= 0) v = ((const uint4*)(a.cf + it * a.ldc))[c];
-      dst = (uint4*)(a.c_cf + (int64_t)p * a.ldc) + c;
+    if (i < n32) {
+      const int p = (int)(i / per32);
+      int c = (int)(i - (int64_t)p * per32);
+      const int64_t item = item_of(p), sl = (int64_t)p * S;
+      if (c < a.ch_items) {
+        v = ((const uint4*)(a.items + item * a.ld))[c];
+        dst = (uint4*)(a.c_items + sl * a.ld) + c;
+      } else {
+        c -= a.ch_items;
+        v = ((const uint4*)(a.cf + item * a.ldc))[c];
+        dst = (uint4*)(a.c_cf + sl * a.ldc) + c;
+      }
     } else {
-      c -= a.ch_cf;
-      if (item >= 0) v = ((const uint4*)(a.cf_bf + it * a.ldc_b))[c];
-      dst = (uint4*)(a.c_cf_bf + (int64_t)p * a.ldc_b) + c;
+      const int64_t j = i - n32;
+      const int sl = (int)(j / per16);
+      if (sl >= a.cap) return;
+      int c = (int)(j - (int64_t)sl * per16);
+      const int64_t item = sl % S ? -1 : item_of(sl / S);
+      const int64_t it = item >= 0 ? item : 0;
+      if (c < a.ch_items_b) {
+        if (item >= 0) v = ((const uint4*)(a.items_bf + it * a.ld_b))[c];
+        dst = (uint4*)(a.c_items_bf + (int64_t)sl * a.ld_b) + c;
+      } else {
+        c -= a.ch_items_b;
+        if (item >= 0) v = ((const uint4*)(a.cf_bf + it * a.ldc_b))[c];
+        dst = (uint4*)(a.c_cf_bf + (int64_t)sl * a.ldc_b) + c;
+      }
     }
     *dst = v;
     return;
@@ -157,7 +174,7 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
         const int64_t r = key ? (int64_t)gid_of(key) - (int64_t)a.id_offset : -1;
         if (r >= 0 && r < a.n && ((mw[r >> 5] >> (r & 31)) & 1u)) {
           const uint32_t p = pre[r >> 5] + (uint32_t)__popc(mw[r >> 5] & ((1u << (r & 31)) - 1u));
-          if (p < E) rowbits[p >> 5] |= 1u << (p & 31);
+          if (p < E) rowbits[(p * S) >> 5] |= 1u << ((p * S) & 31);
         }
       }
       __syncthreads();
@@ -176,7 +193,7 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
         const int bit = __builtin_ctz(hit);
         hit &= hit - 1u;
         const uint32_t p = pre[w] + (uint32_t)__popc(mw[w] & ((1u << bit) - 1u));
-        if (p < E) atomicOr(&rowbits[p >> 5], 1u << (p & 31));
+        if (p < E) atomicOr(&rowbits[(p * S) >> 5], 1u << ((p * S) & 31));
       }
     }
     __syncthreads();
@@ -189,7 +206,8 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
   const int per = a.ch_items + a.ch_items_b + a.ch_cf + a.ch_cf_b;
   if (a.nw <= 0 || a.nw > kCompactMaxWords || a.cap <= 0 || a.cap % 32 || a.cnw * 32 != a.cap ||
       a.cnw > kCompactMaxWords || a.xnw <= 0 || a.xnw > a.cnw || a.n_word_wg != a.cnw || a.B < 0 || per <= 0 ||
-      (int64_t)a.n_copy_wg * kCompactThreads < (int64_t)a.cap * per ||
+      a.stride < 1 || a.cap_pos * a.stride != a.cap ||
+      (int64_t)a.n_copy_wg * kCompactThreads < (int64_t)a.cap_pos * (a.ch_items + a.ch_cf) + (int64_t)a.cap * (a.ch_items_b + a.ch_cf_b) ||
       (a.items && (!a.items_bf || !a.c_items || !a.c_items_bf || !a.c_present || a.ld % 4 || a.ld_b % 8 ||
                    a.ch_items != a.ld / 4 || a.ch_items_b != a.ld_b / 8)) ||
       (!a.items && (a.ch_items || a.ch_items_b)) ||
