@@ -73,7 +73,7 @@ def scan_kernel_info(dtype, width, batch):
     return f"{kern}<uint16_t,{width * 2 // 16}> (bf16 MFMA)", 1.0
 
 
-def roofline(flops_alg, bytes_alg, kernel_us, dtype, kname, mfma_per_flop, traffic):
+def roofline(flops_alg, bytes_alg, kernel_us, dtype, kname, mfma_per_flop, traffic, mfma16=False):
     """Roofline object of one kernel.  The binding ceiling follows SURVEY.md §8(d):
     max(issued MFMA flops / MFMA peak, algorithmic bytes / HBM peak).  `achieved` is the
     binding side's rate: issued MFMA TFLOP/s (algorithmic flops × MFMA flops per algorithmic
@@ -82,7 +82,10 @@ def roofline(flops_alg, bytes_alg, kernel_us, dtype, kname, mfma_per_flop, traff
     t = kernel_us * 1e-6
     alg_tf = flops_alg / t / 1e12
     issued = alg_tf * mfma_per_flop
-    peak_tf = BF16_DENSE_TF if (dtype == "bf16" or mfma_per_flop > 1 or "bf16" in kname or "f16" in kname) else F32_DENSE_TF
+    # mfma16: the search's flops run on a 16-bit MFMA (the f32 index's one-product f16 scan),
+    # so every family of that search is priced against the 16-bit dense peak
+    peak_tf = (BF16_DENSE_TF if (mfma16 or dtype == "bf16" or mfma_per_flop > 1 or "bf16" in kname or "f16" in kname)
+               else F32_DENSE_TF)
     gbs = bytes_alg / t / 1e9
     t_mfma = flops_alg * mfma_per_flop / (peak_tf * 1e12)
     t_hbm = bytes_alg / (HBM_PEAK_GBS * 1e9)
@@ -110,8 +113,8 @@ def family_kernels(workload, dtype, B, scan_name):
     if workload == "c2" and dtype == "f32" and B <= 16:
         return {"gemm": "sq_scan_kernel (approximate f16 MFMA pass, small batch)", "select": "sq_merge_kernel"}
     if workload == "c3":
-        return {"prep": "prep2_kernel", "gemm": scan_name, "select": "select_list_dual_kernel",
-                "finalize": "finalize1_kernel"}
+        return {"prep": "compact_kernel (constraint-first packing of the allowed rows + both sides' query prep)",
+                "gemm": scan_name, "select": "select_list_dual_kernel", "finalize": "finalize1_kernel"}
     return {"prep": "prep_kernel", "gemm": scan_name,
             "select": "select_list_kernel" if dtype == "f32" else "select_kernel", "rerank": "rerank_kernel",
             "finalize": "finalize1_kernel"}
@@ -137,7 +140,7 @@ def scan_read_roofline(B, d, scan_us, n=N_ITEMS, cus=256):
             "source": "profiles/r05_percu_probe.jsonl (tools/percu_probe.hip)"}
 
 
-def dominant_roofline(fam_us, names, flops, alg_bytes, step_us, dtype, scan_mpf, pmc_key):
+def dominant_roofline(fam_us, names, flops, alg_bytes, step_us, dtype, scan_mpf, pmc_key, mfma16=False):
     """roofline object for the kernel family that takes the most device time per step (HIP
     events, bb_get_profile), with SURVEY.md §8(d)'s algorithmic work of one search priced
     against that kernel's time; `step` prices the same work against the whole step (wall time
@@ -145,14 +148,14 @@ def dominant_roofline(fam_us, names, flops, alg_bytes, step_us, dtype, scan_mpf,
     dom = max(fam_us, key=fam_us.get)
     kname = names.get(dom, dom)
     mpf = scan_mpf if dom == "gemm" else 1.0
-    out = roofline(flops, alg_bytes, fam_us[dom], dtype, kname, mpf, load_pmc(pmc_key, dom))
+    out = roofline(flops, alg_bytes, fam_us[dom], dtype, kname, mpf, load_pmc(pmc_key, dom), mfma16)
     out["family"] = dom
     out["step"] = {"us": round(step_us, 3), "achieved_gbs": round(alg_bytes / (step_us * 1e-6) / 1e9, 1),
                    "frac": round(alg_bytes / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                    "note": "algorithmic bytes of one search / wall time per step of the timed window"}
     if "gemm" in fam_us:
         sc = roofline(flops, alg_bytes, fam_us["gemm"], dtype, names.get("gemm", "gemm"), scan_mpf,
-                      load_pmc(pmc_key, "gemm"))
+                      load_pmc(pmc_key, "gemm"), mfma16)
         out["scan"] = {k: sc[k] for k in ("kernel", "kernel_us", "mfma_issued_tflops", "mfma_frac",
                                           "hbm_frac_at_alg_bytes", "traffic")}
     return out
@@ -754,16 +757,17 @@ def main():
                          "launch, bounded per-lane candidate lists; exact f32 re-rank of the candidates in the list select)")
             else:
                 kname = ("scan4_kernel<48,list|f16> + scan4_kernel<8,list|f16> (content d=384 and CF r=50 one-product "
-                         "f16 scans, one launch per side, the CF side at twice the chunks; bounded per-lane candidate "
-                         "lists; exact f32 re-rank of the candidates in the list select)")
+                         "f16 scans over the packed allowed rows (constraint-first: compact_kernel), one launch per "
+                         "side; bounded per-lane candidate lists; exact f32 re-rank of the candidates in the list select)")
     else:
         flops = 2.0 * B * N_ITEMS * DIM
         alg_bytes = N_ITEMS * DIM * es + B * DIM * 4 + B * TOPK * 8    # items + queries + top-K out
         kname, mpf = scan_kernel_info(args.dtype, DIM, B)
     pmc_key = "c3" if hybrid else args.dtype
     step_us = 1e6 * el / args.steps
+    mfma16 = args.dtype == "f32" and not (os.environ.get("BB_AB") and os.environ.get("BB_NO_RR"))
     roof = dominant_roofline(fam_us, family_kernels(args.workload, args.dtype, B, kname), flops, alg_bytes, step_us,
-                             args.dtype, mpf, pmc_key)
+                             args.dtype, mpf, pmc_key, mfma16)
     if args.dtype == "f32" and "gemm" in fam_us:
         # (hybrid: both sides, the CF factors padded to 64 f16 columns in the re-rank copy)
         roof["scan_reads"] = scan_read_roofline(B, DIM + (64 if hybrid else 0), fam_us["gemm"])
@@ -808,7 +812,8 @@ def main():
     del flush
     fam_cold = {k: 1e3 * v["ms"] / n_cold for k, v in prof_c.items() if v["launches"] and k in fam_us}
     dom = roof["family"]
-    rc_ = roofline(flops, alg_bytes, fam_cold[dom], args.dtype, roof["kernel"], mpf if dom == "gemm" else 1.0, None)
+    rc_ = roofline(flops, alg_bytes, fam_cold[dom], args.dtype, roof["kernel"], mpf if dom == "gemm" else 1.0, None,
+                   mfma16)
     roof["cold"] = {"family": dom, "kernel_us": round(fam_cold[dom], 3), "bound": rc_["bound"],
                     "achieved": rc_["achieved"], "unit": rc_["unit"], "frac": rc_["frac"],
                     "hbm_gbs_at_alg_bytes": rc_["hbm_gbs_at_alg_bytes"],

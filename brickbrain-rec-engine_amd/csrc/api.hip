@@ -164,8 +164,10 @@ struct bb_index {
   bool r0_ready = false;
   bb_index* cx = nullptr;          // the shadow (owned; not a live handle)
   bool shadow = false;             // this index is a shadow: no rank-0 drop, final ids via idmap
-  DevBuf idmap, cq_rows, cexcl0, cexcl1;  // shadow: position -> id, liked rows, exclusions
+  DevBuf idmap, cexcl0, cexcl1;           // shadow: slot -> id, content / CF exclusions
   const uint32_t* cur_cexcl = nullptr;    // shadow: the content exclusions of this search
+  bb::CompactArgs cjob{};                 // shadow: the packing launch, issued in place of its prep
+  bool cjob_set = false;
   size_t filled_words = 0;                // shadow: words of ones / zeros filled
 
   bool prof = false;
@@ -211,7 +213,7 @@ void free_buffers(bb_index* x) {
                     &x->cand, &x->cand_cnt, &x->cand_pmax, &x->items3, &x->cf3, &x->items_bf, &x->cf_bf,
                     &x->rr_stats, &x->qf32, &x->qeps, &x->qcf32, &x->qcfeps, &x->qh, &x->qcfh, &x->rr_out, &x->rr_cnt,
                     &x->rr_thr, &x->rr_r0, &x->rr_r0n, &x->trace, &x->rr_flags, &x->lists, &x->r0lists, &x->pilot_top,
-                    &x->sq_top, &x->sq_ptop, &x->sq_ords, &x->r0key, &x->idmap, &x->cq_rows, &x->cexcl0, &x->cexcl1})
+                    &x->sq_top, &x->sq_ptop, &x->sq_ords, &x->r0key, &x->idmap, &x->cexcl0, &x->cexcl1})
     b->release();
   if (x->ovf_host) (void)hipHostFree(x->ovf_host);
   x->ovf_host = nullptr;
@@ -903,7 +905,7 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
   if (need_cf && ((rc = c->cf.ensure((size_t)cap * x->Rpad * 4)) || (rc = c->cf_bf.ensure((size_t)cap * x->Rpad_b * 2)) ||
                   (rc = c->cf_present.ensure(wb))))
     return rc;
-  if (liked && ((rc = c->cq_rows.ensure((size_t)B * x->d * 4)) || (rc = c->cexcl0.ensure((size_t)B * wb)))) return rc;
+  if (liked && (rc = c->cexcl0.ensure((size_t)B * wb))) return rc;
   if (need_cf && d_excl && (rc = c->cexcl1.ensure((size_t)B * wb))) return rc;
   CompactArgs a{};
   a.mask = (const uint32_t*)d_mask;
@@ -946,8 +948,6 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
   a.B = per_query ? B : 0;
   if (liked) {
     a.q_items = (const int64_t*)d_items;
-    a.q_rows = (float*)c->cq_rows.p;
-    a.d = x->d;
     a.r0key = (const uint64_t*)x->r0key.p;
     a.c_excl0 = (uint32_t*)c->cexcl0.p;
   }
@@ -956,7 +956,11 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
     a.excl_ld = a.nw;
     a.c_excl1 = (uint32_t*)c->cexcl1.p;
   }
-  if ((rc = timed(x, K_PREP, s, [&] { return launch_compact(a, s); }))) return rc;
+  // launched by the shadow's search in place of its prep launch, with that prep's arguments
+  // (so the packing and the query prep are one launch, and nothing runs if the shadow's
+  // shapes leave the list / image paths)
+  c->cjob = a;
+  c->cjob_set = true;
   bb_query q2 = *q;
   q2.where = BB_DEVICE;
   q2.stream = s;
@@ -964,16 +968,14 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
   q2.mask_bits = nullptr;
   q2.mask_count = 0;
   q2.excl_bits = need_cf && d_excl ? (const uint32_t*)c->cexcl1.p : nullptr;
-  if (liked) {
-    q2.q_items = nullptr;
-    q2.q_rows = c->cq_rows.p;
-    q2.q_dtype = F32;
-  } else {
-    q2.q_rows = d_rows;
-  }
+  // (liked sets: the ORIGINAL ids — the packing launch's prep gathers their rows from the full
+  // index; the shadow itself never reads them)
+  q2.q_items = liked ? (const int64_t*)d_items : nullptr;
+  q2.q_rows = liked ? nullptr : d_rows;
   q2.q_cf = d_cf;
   c->cur_cexcl = liked ? (const uint32_t*)c->cexcl0.p : nullptr;
   rc = search_locked(c, &q2, res, false);
+  c->cjob_set = false;
   // the shadow's kernels count as this handle's
   for (auto& pe : c->pending) x->pending.push_back(pe);
   c->pending.clear();
@@ -1454,7 +1456,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       return rc;
     // a shadow's ids are mapped by the list / int16-image selects and finalize1 only: any other
     // path leaves it before its first launch (the caller then runs the full search)
-    if (x->shadow && ((need_content && !list_c && !s16_c) || (need_cf && !list_f && !s16_f)))
+    if (x->shadow && (bc < B || (need_content && !list_c && !s16_c) || (need_cf && !list_f && !s16_f)))
       return b0 == 0 ? kNoCompact : fail(BB_E_STATE, "internal: a packed search's later query chunk left the list path");
     // the prep launches of both sides (hybrid) go out as one launch
     const bool prep_c = need_content && !fuse_c && !rrfuse_c && !rraw_c, prep_f = need_cf && !fuse_f && !rrfuse_f;
@@ -1521,7 +1523,23 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
                         (rr_f ? gemm_uses_scan(BF16, bpad, x->Rpad_b) : x->dtype == BF16 && scan_f);
     pa_c.q_perm = perm_c ? perm_kind : 0;
     pa_f.q_perm = perm_f ? perm_kind : 0;
-    if (prep_c && prep_f) {
+    if (x->shadow && x->cjob_set) {
+      // a packed search: the packing launch (compact.hip) runs this prep in its query
+      // workgroups; the liked sets' rows come from the full index by their original ids
+      CompactArgs cj = x->cjob;
+      if (prep_c) {
+        cj.prep_c = pa_c;
+        if (pa_c.item_ids) {
+          cj.prep_c.items = cj.items;
+          cj.prep_c.n_items = cj.n;
+          cj.prep_c.id_offset = cj.id_offset;
+        }
+      }
+      if (prep_f) cj.prep_f = pa_f;
+      cj.n_query_wg = (int32_t)((std::max<int64_t>(bpad, cj.B) + 3) / 4);
+      x->cjob_set = false;
+      if ((rc = timed(x, K_PREP, s, [&] { return launch_compact(cj, s); }))) return rc;
+    } else if (prep_c && prep_f) {
       if ((rc = timed(x, K_PREP, s, [&] { return launch_prep2(pa_c, pa_f, s); }))) return rc;
     } else if (prep_c || prep_f) {
       if ((rc = timed(x, K_PREP, s, [&] { return launch_prep(prep_c ? pa_c : pa_f, s); }))) return rc;

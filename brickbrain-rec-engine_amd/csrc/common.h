@@ -424,6 +424,32 @@ __device__ __forceinline__ int64_t out_id(const uint32_t* idmap, uint32_t g) {
   return idmap ? (int64_t)idmap[g] : (int64_t)g;
 }
 
+
+
+struct PrepArgs {
+  const void* src;          // query rows [B][d] (q_dtype) or null
+  int32_t src_dtype;
+  int64_t src_ld;
+  const int64_t* item_ids;  // global ids (gather from the item matrix) or null
+  int64_t id_offset;
+  const void* items;        // item matrix [Npad][Dpad] index dtype (for gathers)
+  int64_t n_items;
+  int32_t d, Dpad;          // real and padded widths
+  int32_t normalize;        // 1 = divide by L2 norm (sklearn normalize semantics)
+  void* out;                // [Bpad][Dpad] index dtype
+  int32_t out_dtype;
+  int32_t B, Bpad;
+  // re-rank operands (out_dtype == BF16 with out_f32 set): the f32 row [Bpad][Dpad_f] beside
+  // the bf16 operand, and the per-row bound ε of |bf16 dot − f32 dot| against items whose
+  // error statistics are istats (rr_prepare_kernel): ε = E_x·|q̃| + N_x·|q̃−q| + γ·Ñ_x·|q̃|
+  float* out_f32;
+  int32_t Dpad_f;
+  float* eps_out;           // [Bpad]
+  const float* istats;      // [3]: max |x̃−x|, max |x|, max |x̃| over the item rows
+  float* h_out;             // [Bpad] int16 score-image quantum (rr_quantum; eps_out widened), or null
+  int32_t q_perm;           // the bf16 operand in lane order, not row-major: 1 = scan4's (scan4_q_offset), 2 = scan2's
+};
+
 // Constraint-first search (compact.hip): the rows a mask allows, packed.  Positions [0, cap)
 // of the packed buffers; position p holds the p-th allowed item (ascending ids).
 constexpr int kCompactMaxWords = 2048;  // mask words: indexes of up to 65,536 rows
@@ -457,41 +483,18 @@ struct CompactArgs {
   float* c_cf;
   uint16_t* c_cf_bf;
   uint32_t* c_cf_present;
-  int32_t B;                 // query workgroups
-  const int64_t* q_items;    // [B] liked sets (global ids), with q_rows
-  float* q_rows;             // [B][d] their stored f32 rows out, or null
-  int32_t d;
+  int32_t B;                 // query rows with exclusions
+  int32_t n_query_wg;        // query workgroups (4 rows each): >= B / 4 and >= every prep's Bpad / 4
+  const int64_t* q_items;    // [B] liked sets (global ids) — the rank-0 lookups
   const uint64_t* r0key;     // [n + 1] rank-0 key of each item's own row (the unmasked arg-max); [n]: a zero row's
   uint32_t* c_excl0;         // [B][xnw] content exclusion: the rank-0 item's position, or null
   const uint32_t* excl;      // [B][excl_ld] per-query exclusions over local rows, or null
   int64_t excl_ld;
   uint32_t* c_excl1;         // [B][xnw] the same re-indexed to positions, or null
+  PrepArgs prep_c, prep_f;   // the packed search's query prep of each side (Bpad 0: none), run by
+                             // the query workgroups (prep_body.h) in place of its prep launch
 };
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
-
-struct PrepArgs {
-  const void* src;          // query rows [B][d] (q_dtype) or null
-  int32_t src_dtype;
-  int64_t src_ld;
-  const int64_t* item_ids;  // global ids (gather from the item matrix) or null
-  int64_t id_offset;
-  const void* items;        // item matrix [Npad][Dpad] index dtype (for gathers)
-  int64_t n_items;
-  int32_t d, Dpad;          // real and padded widths
-  int32_t normalize;        // 1 = divide by L2 norm (sklearn normalize semantics)
-  void* out;                // [Bpad][Dpad] index dtype
-  int32_t out_dtype;
-  int32_t B, Bpad;
-  // re-rank operands (out_dtype == BF16 with out_f32 set): the f32 row [Bpad][Dpad_f] beside
-  // the bf16 operand, and the per-row bound ε of |bf16 dot − f32 dot| against items whose
-  // error statistics are istats (rr_prepare_kernel): ε = E_x·|q̃| + N_x·|q̃−q| + γ·Ñ_x·|q̃|
-  float* out_f32;
-  int32_t Dpad_f;
-  float* eps_out;           // [Bpad]
-  const float* istats;      // [3]: max |x̃−x|, max |x|, max |x̃| over the item rows
-  float* h_out;             // [Bpad] int16 score-image quantum (rr_quantum; eps_out widened), or null
-  int32_t q_perm;           // the bf16 operand in lane order, not row-major: 1 = scan4's (scan4_q_offset), 2 = scan2's
-};
 
 struct MaskArgs {
   const int32_t* parts;

@@ -24,13 +24,16 @@
 // items, so a per-lane top-5 list of one tile never overflows: when the top-K is a large
 // share of the allowed rows (configs[2]: 101 of ~440), dense packing overflowed most lists
 // and the list select rescored most rows (48 us, r06d).
-//   query workgroups     one per query row: the liked set's stored row (the content query of
-//                        similar / hybrid searches), the content exclusion of its rank-0 item
-//                        (the arg-max of the UNMASKED ranking, :217 — known per item from the
-//                        rank-0 table, so the packed search drops it as the full one does),
-//                        and the query's CF exclusions (rated items, :441-451) re-indexed to
-//                        positions
+//   query workgroups     four query rows each, one wave per row: the query prep of both sides
+//                        (prep_body.h — the liked set's stored row gathered by id from the
+//                        FULL index, the CF user row, the f16 operand in the scan's lane order,
+//                        the f32 row and bound: the packed search launches no prep), the
+//                        content exclusion of the liked set's rank-0 item (the arg-max of the
+//                        UNMASKED ranking, :217 — known per item from the rank-0 table, so the
+//                        packed search drops it as the full one does), and the query's CF
+//                        exclusions (rated items, :441-451) re-indexed to slots
 #include "common.h"
+#include "prep_body.h"
 
 namespace bb {
 
@@ -45,7 +48,7 @@ __device__ __forceinline__ int select_bit(uint32_t w, int p) {
 __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a) {
   __shared__ uint32_t mw[kCompactMaxWords];
   __shared__ uint32_t pre[kCompactMaxWords + 1];
-  __shared__ uint32_t rowbits[kCompactMaxWords];
+  __shared__ uint32_t rowbits[kCompactThreads / 64][kCompactMaxWords];  // query rows: one per wave
   __shared__ uint32_t scan[kCompactThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nw = a.nw;
@@ -158,47 +161,53 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
     return;
   }
 
-  // ---- query row b ----
-  const int b = g - a.n_word_wg - a.n_copy_wg;
-  if (a.q_rows) {  // the liked set's stored row (zero for an id outside the index, as prep's gather)
-    const int64_t lid = a.q_items[b] - (int64_t)a.id_offset;
-    const bool ok = lid >= 0 && lid < a.n;
-    float* dst = a.q_rows + (int64_t)b * a.d;
-    const float* src = a.items + (ok ? lid : 0) * a.ld;
-    for (int c = tid; c < a.d; c += kCompactThreads) dst[c] = ok ? src[c] : 0.f;
-    if (a.c_excl0) {  // the rank-0 item, where it is allowed
-      for (int w = tid; w < a.xnw; w += kCompactThreads) rowbits[w] = 0u;
-      __syncthreads();
-      if (tid == 0) {
-        const uint64_t key = a.r0key[ok ? lid : a.n];  // [n]: a zero row's rank 0
-        const int64_t r = key ? (int64_t)gid_of(key) - (int64_t)a.id_offset : -1;
-        if (r >= 0 && r < a.n && ((mw[r >> 5] >> (r & 31)) & 1u)) {
-          const uint32_t p = pre[r >> 5] + (uint32_t)__popc(mw[r >> 5] & ((1u << (r & 31)) - 1u));
-          if (p < E) rowbits[(p * S) >> 5] |= 1u << ((p * S) & 31);
-        }
+  // ---- query rows [4q, 4q + 4), one wave each: the prep of both sides (prep_body.h, exactly
+  // prep_kernel's — the packed search launches no prep of its own), then the exclusions ----
+  const int gq = g - a.n_word_wg - a.n_copy_wg;
+  if (a.prep_c.Bpad) prep_rows(a.prep_c, gq);
+  if (a.prep_f.Bpad) prep_rows(a.prep_f, gq);
+  const int b = gq * 4 + wave;
+  if (b >= a.B) return;  // (per wave: no block barrier below)
+  uint32_t* rb = rowbits[wave];
+  auto wave_sync = []() __attribute__((always_inline)) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  if (a.c_excl0) {  // the liked set's rank-0 item (its unmasked arg-max), where it is allowed
+    for (int w = lane; w < a.xnw; w += 64) rb[w] = 0u;
+    wave_sync();
+    if (lane == 0) {
+      const int64_t lid = a.q_items[b] - (int64_t)a.id_offset;
+      const bool ok = lid >= 0 && lid < a.n;  // (outside the index: a zero row, as prep's gather)
+      const uint64_t key = a.r0key[ok ? lid : a.n];  // [n]: a zero row's rank 0
+      const int64_t r = key ? (int64_t)gid_of(key) - (int64_t)a.id_offset : -1;
+      if (r >= 0 && r < a.n && ((mw[r >> 5] >> (r & 31)) & 1u)) {
+        const uint32_t p = pre[r >> 5] + (uint32_t)__popc(mw[r >> 5] & ((1u << (r & 31)) - 1u));
+        if (p < E) rb[(p * S) >> 5] |= 1u << ((p * S) & 31);
       }
-      __syncthreads();
-      uint32_t* out = a.c_excl0 + (int64_t)b * a.xnw;
-      for (int w = tid; w < a.xnw; w += kCompactThreads) out[w] = rowbits[w];
-      __syncthreads();
     }
+    wave_sync();
+    uint32_t* out = a.c_excl0 + (int64_t)b * a.xnw;
+    for (int w = lane; w < a.xnw; w += 64) out[w] = rb[w];
+    wave_sync();
   }
-  if (a.c_excl1) {  // the query's exclusions, re-indexed to positions
-    for (int w = tid; w < a.xnw; w += kCompactThreads) rowbits[w] = 0u;
-    __syncthreads();
+  if (a.c_excl1) {  // the query's exclusions (rated items), re-indexed to slots
+    for (int w = lane; w < a.xnw; w += 64) rb[w] = 0u;
+    wave_sync();
     const uint32_t* ex = a.excl + (int64_t)b * a.excl_ld;
-    for (int w = tid; w < nw; w += kCompactThreads) {
+    for (int w = lane; w < nw; w += 64) {
       uint32_t hit = mw[w] & ex[w];
       while (hit) {
         const int bit = __builtin_ctz(hit);
         hit &= hit - 1u;
         const uint32_t p = pre[w] + (uint32_t)__popc(mw[w] & ((1u << bit) - 1u));
-        if (p < E) atomicOr(&rowbits[(p * S) >> 5], 1u << ((p * S) & 31));
+        if (p < E) atomicOr(&rb[(p * S) >> 5], 1u << ((p * S) & 31));
       }
     }
-    __syncthreads();
+    wave_sync();
     uint32_t* out = a.c_excl1 + (int64_t)b * a.xnw;
-    for (int w = tid; w < a.xnw; w += kCompactThreads) out[w] = rowbits[w];
+    for (int w = lane; w < a.xnw; w += 64) out[w] = rb[w];
   }
 }
 
@@ -214,10 +223,11 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
       (a.cf && (!a.cf_bf || !a.c_cf || !a.c_cf_bf || !a.c_cf_present || a.ldc % 4 || a.ldc_b % 8 ||
                 a.ch_cf != a.ldc / 4 || a.ch_cf_b != a.ldc_b / 8)) ||
       (!a.cf && (a.ch_cf || a.ch_cf_b)) ||
-      (a.q_rows && (!a.q_items || !a.items || a.d <= 0 || a.d > a.ld)) || (a.c_excl0 && (!a.q_rows || !a.r0key)) ||
-      (a.c_excl1 && (!a.excl || a.excl_ld < a.nw)))
+      (a.c_excl0 && (!a.q_items || !a.r0key)) || (a.c_excl1 && (!a.excl || a.excl_ld < a.nw)) ||
+      a.n_query_wg * 4 < a.B || (a.prep_c.Bpad && a.prep_c.Bpad > 4 * a.n_query_wg) ||
+      (a.prep_f.Bpad && a.prep_f.Bpad > 4 * a.n_query_wg))
     return hipErrorInvalidValue;
-  bb_launch(compact_kernel, dim3(a.n_word_wg + a.n_copy_wg + a.B), dim3(kCompactThreads), 0, s, a);
+  bb_launch(compact_kernel, dim3(a.n_word_wg + a.n_copy_wg + a.n_query_wg), dim3(kCompactThreads), 0, s, a);
   return hipGetLastError();
 }
 
