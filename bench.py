@@ -113,8 +113,9 @@ def family_kernels(workload, dtype, B, scan_name):
     if workload == "c2" and dtype == "f32" and B <= 16:
         return {"gemm": "sq_scan_kernel (approximate f16 MFMA pass, small batch)", "select": "sq_merge_kernel"}
     if workload == "c3":
-        return {"prep": "compact_kernel (constraint-first packing of the allowed rows + both sides' query prep)",
-                "gemm": scan_name, "select": "select_list_dual_kernel", "finalize": "finalize1_kernel"}
+        return {"pack": "compact_kernel (constraint-first packing of the allowed rows + both sides' query prep)",
+                "prep": "prep2_kernel", "gemm": scan_name, "select": "select_list_dual_kernel",
+                "finalize": "finalize1_kernel"}
     return {"prep": "prep_kernel", "gemm": scan_name,
             "select": "select_list_kernel" if dtype == "f32" else "select_kernel", "rerank": "rerank_kernel",
             "finalize": "finalize1_kernel"}

@@ -46,8 +46,8 @@ int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 size_t elem_size(int dtype) { return dtype == F64 ? 8 : dtype == BF16 ? 2 : 4; }
 
 // K_RERUN counts searches the streaming path handed back to the slab path (no kernel time)
-enum Kfam { K_PREP = 0, K_GEMM = 1, K_SELECT = 2, K_FIN = 3, K_MASK = 4, K_RERUN = 5, K_RERANK = 6, K_NFAM = 7 };
-const char* kFamNames[K_NFAM] = {"prep", "gemm", "select", "finalize", "mask", "rerun", "rerank"};
+enum Kfam { K_PREP = 0, K_GEMM = 1, K_SELECT = 2, K_FIN = 3, K_MASK = 4, K_RERUN = 5, K_RERANK = 6, K_PACK = 7, K_NFAM = 8 };
+const char* kFamNames[K_NFAM] = {"prep", "gemm", "select", "finalize", "mask", "rerun", "rerank", "pack"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -1538,7 +1538,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       if (prep_f) cj.prep_f = pa_f;
       cj.n_query_wg = (int32_t)((std::max<int64_t>(bpad, cj.B) + 3) / 4);
       x->cjob_set = false;
-      if ((rc = timed(x, K_PREP, s, [&] { return launch_compact(cj, s); }))) return rc;
+      if ((rc = timed(x, K_PACK, s, [&] { return launch_compact(cj, s); }))) return rc;
     } else if (prep_c && prep_f) {
       if ((rc = timed(x, K_PREP, s, [&] { return launch_prep2(pa_c, pa_f, s); }))) return rc;
     } else if (prep_c || prep_f) {

@@ -184,7 +184,7 @@ int bb_finalize(bb_index* idx, const bb_query* q, const uint64_t* keys, const ui
 
 /* Profiling: when enabled, per-kernel HIP events are recorded on the launch stream;
  * bb_get_profile synchronises and returns the accumulated device time and launch count
- * of each kernel family, then clears them. names: "prep","gemm","select","blend","mask". */
+ * of each kernel family, then clears them. names: "prep","gemm","select","finalize","mask","rerun","rerank","pack" (the constraint-first packing launch). */
 typedef struct {
   double ms[8];
   int64_t launches[8];

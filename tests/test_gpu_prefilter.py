@@ -2,7 +2,7 @@
 packed and only they are searched — the reference's "apply hard constraints first"
 (recommendation_system.py:628-656).  Every case runs the same search with the prefilter forced
 on and off and asserts identical bits (ids, scores, counts), and checks that the packed path
-actually ran (one more "prep"-family launch: the packing kernel).
+actually ran (one "pack"-family launch: the packing kernel, which also runs the query prep).
 
 Cases: every mode (semantic, similar with rank-0 inside and outside the mask, CF with rated
 exclusions, hybrid), masks of 0.1 % .. 25 %, an empty mask, exact duplicates of liked rows (the
@@ -51,7 +51,7 @@ def _both(idx, mode, k, **kw):
         out[opt] = idx.search(mode, k, **kw)
         prof = idx.profile()
         idx.set_profiling(False)
-        out[f"prep{opt}"] = prof["prep"]["launches"]
+        out[f"pack{opt}"] = prof["pack"]["launches"]
     idx.set_option("prefilter", -1)
     return out
 
@@ -61,7 +61,7 @@ def _same(o, B):
     assert np.array_equal(c0, c1), (c0[:8], c1[:8])
     assert np.array_equal(i0, i1), np.flatnonzero((i0 != i1).any(1))[:8]
     assert np.array_equal(s0.view(np.uint32), s1.view(np.uint32))
-    assert o["prep1"] == o["prep0"] + 1, (o["prep0"], o["prep1"])   # the packing kernel ran
+    assert (o["pack0"], o["pack1"]) == (0, 1), (o["pack0"], o["pack1"])   # the packing kernel ran
 
 
 @pytest.mark.parametrize("density", [0.001, 0.0175, 0.1, 0.25])
