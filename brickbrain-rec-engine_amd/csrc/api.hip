@@ -878,6 +878,7 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
                      : (int64_t)K_int * 16 >= e1                    ? 2
                                                                     : 1;
   const int64_t cap = round_up(e1 * stride, kTileRows);
+  if (cap > kCompactMaxSlots) return kNoCompact;  // (forced on a dense mask: the full search)
   const int cnw = (int)(cap / 32);
   c->n = e1 * stride;
   c->Npad = cap;
@@ -1536,7 +1537,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         }
       }
       if (prep_f) cj.prep_f = pa_f;
-      cj.n_query_wg = (int32_t)((std::max<int64_t>(bpad, cj.B) + 3) / 4);
+      cj.n_excl_wg = (cj.B + 3) / 4;
       x->cjob_set = false;
       if ((rc = timed(x, K_PACK, s, [&] { return launch_compact(cj, s); }))) return rc;
     } else if (prep_c && prep_f) {

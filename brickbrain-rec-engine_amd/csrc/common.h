@@ -452,7 +452,8 @@ struct PrepArgs {
 
 // Constraint-first search (compact.hip): the rows a mask allows, packed.  Positions [0, cap)
 // of the packed buffers; position p holds the p-th allowed item (ascending ids).
-constexpr int kCompactMaxWords = 2048;  // mask words: indexes of up to 65,536 rows
+constexpr int kCompactMaxWords = 2048;   // mask words: indexes of up to 65,536 rows
+constexpr int kCompactMaxSlots = 16384;  // packed slots (the auto rule packs at most n / 4 rows)
 struct CompactArgs {
   const uint32_t* mask;      // [nw] allowed items (device)
   int64_t n;                 // items of the index
@@ -484,7 +485,7 @@ struct CompactArgs {
   uint16_t* c_cf_bf;
   uint32_t* c_cf_present;
   int32_t B;                 // query rows with exclusions
-  int32_t n_query_wg;        // query workgroups (4 rows each): >= B / 4 and >= every prep's Bpad / 4
+  int32_t n_excl_wg;         // exclusion workgroups (4 rows each): ceil(B / 4), 0 without exclusions
   const int64_t* q_items;    // [B] liked sets (global ids) — the rank-0 lookups
   const uint64_t* r0key;     // [n + 1] rank-0 key of each item's own row (the unmasked arg-max); [n]: a zero row's
   uint32_t* c_excl0;         // [B][xnw] content exclusion: the rank-0 item's position, or null

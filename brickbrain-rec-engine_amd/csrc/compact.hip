@@ -11,8 +11,8 @@
 // pipeline runs over the packed rows.  Scores are computed from bit-identical operands, so the
 // results are identical to the full scan's.
 //
-// One launch, three kinds of workgroup (every one first builds the popcount prefix of the mask
-// words in LDS — ≤ 2,048 words, L2-resident — so no workgroup waits for another):
+// One launch, four kinds of workgroup (all but the prep ones first build the popcount prefix of
+// the mask words in LDS — ≤ 2,048 words, L2-resident — so no workgroup waits for another):
 //   word workgroups      32 positions each: the id map and the present words of both item
 //                        spaces
 //   copy workgroups      one 16-B piece per thread of the packed rows (f32 + f16 content, f32 +
@@ -24,14 +24,15 @@
 // items, so a per-lane top-5 list of one tile never overflows: when the top-K is a large
 // share of the allowed rows (configs[2]: 101 of ~440), dense packing overflowed most lists
 // and the list select rescored most rows (48 us, r06d).
-//   query workgroups     four query rows each, one wave per row: the query prep of both sides
-//                        (prep_body.h — the liked set's stored row gathered by id from the
-//                        FULL index, the CF user row, the f16 operand in the scan's lane order,
-//                        the f32 row and bound: the packed search launches no prep), the
-//                        content exclusion of the liked set's rank-0 item (the arg-max of the
-//                        UNMASKED ranking, :217 — known per item from the rank-0 table, so the
-//                        packed search drops it as the full one does), and the query's CF
-//                        exclusions (rated items, :441-451) re-indexed to slots
+//   exclusion workgroups four query rows each, one wave per row: the content exclusion of the
+//                        liked set's rank-0 item (the arg-max of the UNMASKED ranking, :217 —
+//                        known per item from the rank-0 table, so the packed search drops it as
+//                        the full one does) and the query's CF exclusions (rated items,
+//                        :441-451) re-indexed to slots
+//   prep workgroups      four query rows of one side each (no mask prefix): prep_kernel's body
+//                        (prep_body.h — the liked set's stored row gathered by id from the FULL
+//                        index, the CF user row; the f16 operand in the scan's lane order, the
+//                        f32 row and bound), so the packed search launches no prep
 #include "common.h"
 #include "prep_body.h"
 
@@ -48,10 +49,21 @@ __device__ __forceinline__ int select_bit(uint32_t w, int p) {
 __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a) {
   __shared__ uint32_t mw[kCompactMaxWords];
   __shared__ uint32_t pre[kCompactMaxWords + 1];
-  __shared__ uint32_t rowbits[kCompactThreads / 64][kCompactMaxWords];  // query rows: one per wave
+  __shared__ uint32_t rowbits[kCompactThreads / 64][kCompactMaxSlots / 32];  // exclusion rows: one per wave
   __shared__ uint32_t scan[kCompactThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nw = a.nw;
+  const int g = blockIdx.x;
+  // ---- query prep workgroups (no mask prefix needed): four rows of one side each, one wave
+  // per row — prep_kernel's body (prep_body.h), so the packed search launches no prep ----
+  {
+    const int g0 = a.n_word_wg + a.n_copy_wg + a.n_excl_wg, nc = a.prep_c.Bpad / 4, nf = a.prep_f.Bpad / 4;
+    if (g >= g0) {
+      if (g < g0 + nc) prep_rows(a.prep_c, g - g0);
+      else if (g < g0 + nc + nf) prep_rows(a.prep_f, g - g0 - nc);
+      return;
+    }
+  }
   // ---- mask words (bits past n cleared) and their exclusive popcount prefix ----
   constexpr int kWpt = kCompactMaxWords / kCompactThreads;
   uint32_t cnt[kWpt];
@@ -105,7 +117,6 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
     return (int64_t)lo * 32 + select_bit(mw[lo], p - (int)pre[lo]);
   };
 
-  const int g = blockIdx.x;
   if (g < a.n_word_wg) {
     // ---- slots [32g, 32g + 32): the id map and one present word per item space ----
     if (wave == 0) {
@@ -161,11 +172,8 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
     return;
   }
 
-  // ---- query rows [4q, 4q + 4), one wave each: the prep of both sides (prep_body.h, exactly
-  // prep_kernel's — the packed search launches no prep of its own), then the exclusions ----
+  // ---- exclusion rows [4q, 4q + 4), one wave each ----
   const int gq = g - a.n_word_wg - a.n_copy_wg;
-  if (a.prep_c.Bpad) prep_rows(a.prep_c, gq);
-  if (a.prep_f.Bpad) prep_rows(a.prep_f, gq);
   const int b = gq * 4 + wave;
   if (b >= a.B) return;  // (per wave: no block barrier below)
   uint32_t* rb = rowbits[wave];
@@ -214,7 +222,7 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
   const int per = a.ch_items + a.ch_items_b + a.ch_cf + a.ch_cf_b;
   if (a.nw <= 0 || a.nw > kCompactMaxWords || a.cap <= 0 || a.cap % 32 || a.cnw * 32 != a.cap ||
-      a.cnw > kCompactMaxWords || a.xnw <= 0 || a.xnw > a.cnw || a.n_word_wg != a.cnw || a.B < 0 || per <= 0 ||
+      a.cap > kCompactMaxSlots || a.xnw <= 0 || a.xnw > a.cnw || a.n_word_wg != a.cnw || a.B < 0 || per <= 0 ||
       a.stride < 1 || a.cap_pos * a.stride != a.cap ||
       (int64_t)a.n_copy_wg * kCompactThreads < (int64_t)a.cap_pos * (a.ch_items + a.ch_cf) + (int64_t)a.cap * (a.ch_items_b + a.ch_cf_b) ||
       (a.items && (!a.items_bf || !a.c_items || !a.c_items_bf || !a.c_present || a.ld % 4 || a.ld_b % 8 ||
@@ -224,10 +232,10 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
                 a.ch_cf != a.ldc / 4 || a.ch_cf_b != a.ldc_b / 8)) ||
       (!a.cf && (a.ch_cf || a.ch_cf_b)) ||
       (a.c_excl0 && (!a.q_items || !a.r0key)) || (a.c_excl1 && (!a.excl || a.excl_ld < a.nw)) ||
-      a.n_query_wg * 4 < a.B || (a.prep_c.Bpad && a.prep_c.Bpad > 4 * a.n_query_wg) ||
-      (a.prep_f.Bpad && a.prep_f.Bpad > 4 * a.n_query_wg))
+      a.n_excl_wg * 4 < a.B || (a.B && !a.c_excl0 && !a.c_excl1) || a.prep_c.Bpad % 4 || a.prep_f.Bpad % 4)
     return hipErrorInvalidValue;
-  bb_launch(compact_kernel, dim3(a.n_word_wg + a.n_copy_wg + a.n_query_wg), dim3(kCompactThreads), 0, s, a);
+  bb_launch(compact_kernel, dim3(a.n_word_wg + a.n_copy_wg + a.n_excl_wg + (a.prep_c.Bpad + a.prep_f.Bpad) / 4),
+            dim3(kCompactThreads), 0, s, a);
   return hipGetLastError();
 }
 
