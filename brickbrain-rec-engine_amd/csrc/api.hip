@@ -195,6 +195,7 @@ struct bb_plan {
   std::mutex mu;
   hipEvent_t done = nullptr;
   bool launched = false;
+  bool unevented = false;  // replayed without the event (A/B runs)
   std::vector<bb::CapturedOp> ops;
   std::vector<std::vector<void*>> argv;  // per launch: pointers into its argument blob
 };
@@ -2361,8 +2362,11 @@ int bb_plan_launch(bb_plan* p) {
       return fail(BB_E_HIP, std::string("bb_plan_launch: ") + hipGetErrorString(e));
     }
   }
-  const hipError_t e = hipEventRecord(p->done, p->s);
-  p->launched = p->launched || e == hipSuccess;
+  // (BB_PLAN_EVENT=0, A/B runs only: no completion event — destroy then waits for the device)
+  static const bool no_event = ab_env("BB_PLAN_EVENT") && atoi(ab_env("BB_PLAN_EVENT")) == 0;
+  const hipError_t e = no_event ? hipSuccess : hipEventRecord(p->done, p->s);
+  p->launched = p->launched || (e == hipSuccess && !no_event);
+  p->unevented = p->unevented || no_event;
   if (cur >= 0 && cur != p->device) (void)hipSetDevice(cur);
   if (e != hipSuccess) return fail(BB_E_HIP, std::string("bb_plan_launch: hipEventRecord: ") + hipGetErrorString(e));
   return BB_OK;
@@ -2378,6 +2382,7 @@ int bb_plan_destroy(bb_plan* p) {
     // the replays ran on the caller's stream, which may be gone by now: wait for the last
     // replay's event (recorded after its launches), not for the whole device
     if (p->launched) (void)hipEventSynchronize(p->done);
+    if (p->unevented) (void)hipDeviceSynchronize();
     (void)hipEventDestroy(p->done);
   }
   const int rc = bb_destroy(p->view);
