@@ -358,6 +358,7 @@ class ItemIndex:
                torch.empty((B,), dtype=torch.int32, device=dev))
         s = stream if stream is not None else torch.cuda.current_stream(dev)
         keep = [t for t in (q_rows, q_items, q_cf, mask, excl) if t is not None]
+        keep.append(s)  # a plan's stream must outlive it (bb_plan_destroy synchronises it)
         q = self._query(mode, k, B, k_side, L.BB_DEVICE,
                         q_rows.data_ptr() if q_rows is not None else None,
                         _torch_dtype_code(q_rows) if q_rows is not None else 0,
@@ -412,6 +413,7 @@ class ItemIndex:
         maxk = torch.zeros((B,), dtype=torch.int64, device=dev)
         s = stream if stream is not None else torch.cuda.current_stream(dev)
         keep = [t for t in (q_rows, q_items, q_cf, mask, excl) if t is not None]
+        keep.append(s)  # a plan's stream must outlive it (bb_plan_destroy synchronises it)
         q = self._query(mode, k, B, k_side, L.BB_DEVICE,
                         q_rows.data_ptr() if q_rows is not None else None,
                         _torch_dtype_code(q_rows) if q_rows is not None else 0,

@@ -190,12 +190,10 @@ struct bb_plan {
   hipStream_t s = nullptr;
   // launches of one plan from several threads are serialised by mu (two replays'
   // launches interleaved on one stream would let one overwrite the other's scratch between
-  // producer and consumer); `done` is recorded after each replay, so destroy waits for the
-  // plan's own work only (the stream may be the caller's, gone by then: the event stays valid)
+  // producer and consumer).  Destroy waits for the plan's stream s only (the caller keeps it
+  // valid until then, include/brickrec.h), not for the device.  (An event recorded after each
+  // replay instead cost +2.7 us per one-query plan, r06g: similar_k10 19.8 -> 22.4 us.)
   std::mutex mu;
-  hipEvent_t done = nullptr;
-  bool launched = false;
-  bool unevented = false;  // replayed without the event (A/B runs)
   std::vector<bb::CapturedOp> ops;
   std::vector<std::vector<void*>> argv;  // per launch: pointers into its argument blob
 };
@@ -2319,14 +2317,6 @@ int bb_plan_create(bb_index* x, const bb_query* q, const bb_result* res, bb_plan
     g_err = msg;
     return rc == kRetrySlab ? BB_E_HOSTSYNC : rc;
   }
-  // completion only (destroy frees the view after it): no system-scope release fence — with
-  // the default flags each replay's event wrote back and invalidated the caches, +5 us on a
-  // one-query plan (r06b plan_latency: similar_k10 19.6 -> 24.5 us)
-  if (hipEventCreateWithFlags(&p->done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
-    delete p;
-    (void)bb_destroy(v);
-    return fail(BB_E_HIP, "bb_plan_create: hipEventCreateWithFlags failed");
-  }
   p->argv.resize(p->ops.size());
   for (size_t i = 0; i < p->ops.size(); ++i)
     for (uint32_t o : p->ops[i].offs) p->argv[i].push_back(p->ops[i].blob.data() + o);
@@ -2362,13 +2352,7 @@ int bb_plan_launch(bb_plan* p) {
       return fail(BB_E_HIP, std::string("bb_plan_launch: ") + hipGetErrorString(e));
     }
   }
-  // (BB_PLAN_EVENT=0, A/B runs only: no completion event — destroy then waits for the device)
-  static const bool no_event = ab_env("BB_PLAN_EVENT") && atoi(ab_env("BB_PLAN_EVENT")) == 0;
-  const hipError_t e = no_event ? hipSuccess : hipEventRecord(p->done, p->s);
-  p->launched = p->launched || (e == hipSuccess && !no_event);
-  p->unevented = p->unevented || no_event;
   if (cur >= 0 && cur != p->device) (void)hipSetDevice(cur);
-  if (e != hipSuccess) return fail(BB_E_HIP, std::string("bb_plan_launch: hipEventRecord: ") + hipGetErrorString(e));
   return BB_OK;
 }
 
@@ -2379,11 +2363,9 @@ int bb_plan_destroy(bb_plan* p) {
   {
     std::lock_guard<std::mutex> pl(p->mu);  // a launch that passed its check finishes enqueueing
     DeviceGuard g(p->device);
-    // the replays ran on the caller's stream, which may be gone by now: wait for the last
-    // replay's event (recorded after its launches), not for the whole device
-    if (p->launched) (void)hipEventSynchronize(p->done);
-    if (p->unevented) (void)hipDeviceSynchronize();
-    (void)hipEventDestroy(p->done);
+    // the replays ran on the plan's stream (the caller's, valid until now by contract): wait
+    // for it, not for the whole device
+    (void)hipStreamSynchronize(p->s);
   }
   const int rc = bb_destroy(p->view);
   p->magic = 0;

@@ -263,8 +263,9 @@ int bb_create_view(bb_index* base, bb_index** out);
  * bb_search for those; any other refusal is an error.  One plan may be launched from several
  * threads: bb_plan_launch holds the plan's lock while it enqueues, so two replays never
  * interleave their launches on the plan's workspace (they still share it: the second replay
- * queues behind the first on the stream).  bb_plan_destroy waits for the plan's last replay
- * (an event recorded after each launch), not for the whole device, then releases the view. */
+ * queues behind the first on the stream).  The plan's stream must stay valid until
+ * bb_plan_destroy, which waits for that stream (not for the whole device), then releases the
+ * view. */
 typedef struct bb_plan bb_plan;
 int bb_plan_create(bb_index* idx, const bb_query* q, const bb_result* res, bb_plan** out);
 int bb_plan_launch(bb_plan* plan);
