@@ -266,8 +266,10 @@ __device__ __forceinline__ float s16_hi(uint32_t w, float h) { return (float)(in
 // Item chunks of a query-resident scan launch (shared by the launcher and the host code
 // sizing the streaming candidate regions): one workgroup per CU, ~256 workgroups.
 inline int scan_n_chunks(int Mpad, int tiles) {
+  // BB_SCAN_WG (A/B runs): the workgroup count aimed at (default one per CU)
+  static const int wg = ab_env("BB_SCAN_WG") ? std::atoi(ab_env("BB_SCAN_WG")) : 256;
   const int n_groups = Mpad / 128;
-  int n_chunks = (256 + n_groups - 1) / n_groups;
+  int n_chunks = (wg + n_groups - 1) / n_groups;
   return n_chunks < tiles ? n_chunks : tiles;
 }
 
