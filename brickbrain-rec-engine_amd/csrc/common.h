@@ -265,9 +265,16 @@ __device__ __forceinline__ float s16_hi(uint32_t w, float h) { return (float)(in
 
 // Item chunks of a query-resident scan launch (shared by the launcher and the host code
 // sizing the streaming candidate regions): one workgroup per CU, ~256 workgroups.
-inline int scan_n_chunks(int Mpad, int tiles) {
-  // BB_SCAN_WG (A/B runs): the workgroup count aimed at (default one per CU)
-  static const int wg = ab_env("BB_SCAN_WG") ? std::atoi(ab_env("BB_SCAN_WG")) : 256;
+// wg: workgroups aimed at.  The list scans of the exact re-rank path (one slab of an f32
+// index, batches in flight: scan2 holds one workgroup per CU with the whole register file)
+// aim at 224 — four CUs per XCD left to the other lanes' prep / list select, which otherwise
+// wait for the scan to drain: configs[1] 14.1-14.3 -> 15.1-15.5 M q/s on 500 steps, the
+// driver's 20 steps 12.1-12.6 -> 13.2-14.6, the scan itself 12.3 -> 13.3 us (r06h, r06h2:
+// 232 and 240 gave nothing, 208-216 the same as 224).  BB_SCAN_WG (A/B runs) overrides it.
+constexpr int kScanListWg = 224;
+inline int scan_n_chunks(int Mpad, int tiles, int wg = 256) {
+  static const int wg_env = ab_env("BB_SCAN_WG") ? std::atoi(ab_env("BB_SCAN_WG")) : 0;
+  if (wg_env > 0 && wg != 256) wg = wg_env;
   const int n_groups = Mpad / 128;
   int n_chunks = (wg + n_groups - 1) / n_groups;
   return n_chunks < tiles ? n_chunks : tiles;

@@ -56,7 +56,8 @@ static void launch_scan_t(const GemmArgs& a, hipStream_t s) {
   const int n_groups = a.Mpad / (kScanWaves * 32);
   const int tiles = a.Ncols / 32;
   // one workgroup per CU (LDS + VGPR budget): ~256 workgroups, chunks balanced to ±1 tile
-  const int n_chunks = scan_n_chunks(a.Mpad, tiles);
+  // (list scans: kScanListWg, common.h — the host's list geometry uses the same count)
+  const int n_chunks = scan_n_chunks(a.Mpad, tiles, a.lists ? kScanListWg : 256);
   if constexpr (sizeof(T) == 2 && KU <= kRrMaxD / 8) {
     // the exact re-rank path: the f16 copy of an f32 index (launch_gemm checked a.f16)
     if (a.lists) {  // bounded candidate lists

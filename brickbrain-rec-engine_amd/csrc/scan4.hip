@@ -21,7 +21,7 @@ bool scan4_used(int dtype, int Mpad) {
 }
 
 int scan_chunks(int dtype, int Mpad, int tiles, bool split, int list_ku) {
-  if (split || !scan4_used(dtype, Mpad)) return scan_n_chunks(Mpad, tiles);
+  if (split || !scan4_used(dtype, Mpad)) return scan_n_chunks(Mpad, tiles, list_ku > 0 ? kScanListWg : 256);
   return list_ku > 0 ? scan4_list_chunks(Mpad, tiles, list_ku) : scan4_n_chunks(Mpad, tiles);
 }
 
