@@ -354,7 +354,7 @@ def run_sharded(args, rank, world, local, dev):
     q = unit_rows_torch(B, d, 4321, dev)                      # replicated batch
 
     def step():
-        return sh.search("semantic", k, q_rows=q)
+        return sh.search("semantic", k, q_rows=q, pipeline=args.pipeline)
 
     for _ in range(args.warmup):
         step()
@@ -643,6 +643,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="device-free rehearsal of the launcher and the reporting path (gloo ranks, no GPU)")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU-baseline timing")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="sharded workloads: query chunks whose key all-gathers overlap the next chunk's search")
     ap.add_argument("--mall-flush", action="store_true",
                     help="flush the 256 MiB Infinity Cache before every timed step (cold-MALL profiling runs; "
                          "use with --inflight 1 under rocprofv3)")

@@ -50,16 +50,37 @@ def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
     return lo, min(n, lo + per)
 
 
-def _all_gather(t, group, world):
-    """Gather equal-shape tensors -> [world, *t.shape] (one buffer with nccl/RCCL)."""
+def _all_gather(t, group, world, async_op=False):
+    """Gather equal-shape tensors -> [world, *t.shape] (one buffer with nccl/RCCL).  With
+    async_op the collective is only enqueued (RCCL: on its own stream, after the work already
+    on the current stream) and (out, work) comes back; work.wait() orders the current stream
+    after it."""
     import torch
     import torch.distributed as dist
     out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
     if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+        w = dist.all_gather_into_tensor(out, t.contiguous(), group=group, async_op=async_op)
     else:
-        dist.all_gather(list(out.unbind(0)), t.contiguous(), group=group)
-    return out
+        w = dist.all_gather(list(out.unbind(0)), t.contiguous(), group=group, async_op=async_op)
+    return (out, w) if async_op else out
+
+
+def _gather_lists(keys, maxk, group, world, async_op=False):
+    """The merge's one exchange: the key lists [sides, B, k_int] and max keys [B] of every
+    rank as ONE all-gather of a packed int64 buffer (round 6: was two collectives).  Returns a
+    function giving ([P, sides, B, k_int], [P, B]) once the gather has landed."""
+    import torch
+    nk = keys.numel()
+    flat = torch.cat([keys.reshape(-1), maxk.reshape(-1)])
+    res = _all_gather(flat, group, world, async_op)
+    out, work = res if async_op else (res, None)
+
+    def finish():
+        if work is not None:
+            work.wait()
+        return (out[:, :nk].reshape((world,) + tuple(keys.shape)).contiguous(),
+                out[:, nk:].reshape(world, maxk.shape[0]).contiguous())
+    return finish
 
 
 class ShardedIndex:
@@ -217,12 +238,30 @@ class ShardedIndex:
         return getattr(self.local, "torch_device", None) or (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
 
+    def _local_keys(self, mode, k, q_rows, q_cf, loc_mask, loc_excl, k_side):
+        import torch
+        if self.empty:   # no rows here: empty lists (key 0) for the gather
+            sides, kint = self.local.key_lens(mode, k, k_side)
+            B = int((q_rows if q_rows is not None else q_cf).shape[0])
+            dev = self._device()
+            return (torch.zeros((sides, B, kint), dtype=torch.int64, device=dev),
+                    torch.zeros((B,), dtype=torch.int64, device=dev))
+        return self.local.search_keys(mode, k, q_rows=q_rows, q_cf=q_cf, mask=loc_mask, excl=loc_excl,
+                                      k_side=k_side)
+
     def search(self, mode: str, k: int, *, q_rows=None, q_items=None, q_cf=None, mask=None, excl=None,
-               k_side: int = 0, w_content: float = 0.4, w_cf: float = 0.6):
+               k_side: int = 0, w_content: float = 0.4, w_cf: float = 0.6, pipeline: int = 1):
         """Global top-k for a replicated batch; every rank returns the same results.
         mask: this rank's device bitset (``mask_bits``: int32 [words]) — or a global bool [N]
         for small cases; excl: this rank's [B, words] device bitset (``excl_bits``) — or a
-        global bool [B, N]."""
+        global bool [B, N].
+
+        pipeline = c > 1 splits the batch into c query chunks: chunk i's key gather is
+        enqueued asynchronously (RCCL's own stream) and overlaps chunk i+1's local search
+        (the all-gather overlapped with the last tiles).  Results are identical for
+        every c (each query's merge is independent).  Opt-in: each chunk pays the streaming
+        search's fixed costs (pilot, candidate selects, launches) again, and no 8-GPU run has
+        measured the trade here."""
         import torch
         dev = self._device()
         if mode in ("similar", "hybrid") and q_rows is None:
@@ -231,15 +270,23 @@ class ShardedIndex:
         loc_excl = self._local_bits(excl, True)
         q_rows = None if q_rows is None else torch.as_tensor(q_rows).to(dev).float().contiguous()
         q_cf = None if q_cf is None else torch.as_tensor(q_cf).to(dev).float().contiguous()
-        if self.empty:   # no rows here: empty lists (key 0) for the gather
-            sides, kint = self.local.key_lens(mode, k, k_side)
-            B = int((q_rows if q_rows is not None else q_cf).shape[0])
-            keys = torch.zeros((sides, B, kint), dtype=torch.int64, device=dev)
-            maxk = torch.zeros((B,), dtype=torch.int64, device=dev)
-        else:
-            keys, maxk = self.local.search_keys(mode, k, q_rows=q_rows, q_cf=q_cf, mask=loc_mask,
-                                                excl=loc_excl, k_side=k_side)
-        all_keys = _all_gather(keys, self.group, self.world)   # [P, sides, B, k_int]
-        all_max = _all_gather(maxk, self.group, self.world)    # [P, B]
-        return self.local.finalize(mode, k, all_keys, all_max, self.world, k_side=k_side,
-                                   w_content=w_content, w_cf=w_cf)
+        B = int((q_rows if q_rows is not None else q_cf).shape[0])
+        c = max(1, min(int(pipeline), B))
+        bounds = [(B * i // c, B * (i + 1) // c) for i in range(c)]
+        pending = []
+        for lo, hi in bounds:
+            sl = slice(lo, hi)
+            keys, maxk = self._local_keys(mode, k, None if q_rows is None else q_rows[sl],
+                                          None if q_cf is None else q_cf[sl], loc_mask,
+                                          None if loc_excl is None else loc_excl[sl].contiguous(), k_side)
+            pending.append(_gather_lists(keys, maxk, self.group, self.world, async_op=c > 1))
+        outs = []
+        for finish in pending:
+            all_keys, all_max = finish()                                    # [P, sides, b, k_int], [P, b]
+            outs.append(self.local.finalize(mode, k, all_keys, all_max, self.world, k_side=k_side,
+                                            w_content=w_content, w_cf=w_cf))
+        if c == 1:
+            return outs[0]
+        if isinstance(outs[0][0], torch.Tensor):
+            return tuple(torch.cat([o[i] for o in outs], 0) for i in range(3))
+        return tuple(np.concatenate([o[i] for o in outs], 0) for i in range(3))

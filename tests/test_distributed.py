@@ -63,6 +63,11 @@ def _worker(rank, world, port, out_q):
         res["similar/bits"] = si.search("similar", K, q_items=items, mask=mb)
         res["cf/bits"] = si.search("cf", K, q_cf=torch.from_numpy(u), excl=eb, mask=mb)
         res["hybrid/bits"] = si.search("hybrid", K, q_items=items, q_cf=torch.from_numpy(u), excl=eb, mask=mb)
+        # pipelined merge (query chunks, each chunk's key gather in flight behind the next
+        # chunk's local search): the same lists for every chunking
+        res["semantic/pipe2"] = si.search("semantic", K, q_rows=torch.from_numpy(q), mask=mb, pipeline=2)
+        res["hybrid/pipe3"] = si.search("hybrid", K, q_items=items, q_cf=torch.from_numpy(u), excl=eb, mask=mb,
+                                        pipeline=3)
         out_q.put((rank, {m: tuple(t.numpy() for t in v) for m, v in res.items()}))
     finally:
         dist.destroy_process_group()

@@ -14,6 +14,14 @@ for w in $WL; do
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$O/prof_$w" -o run \
       --output-format csv -- python3 "$R/bench.py" --no-cpu --no-sweep --inflight 1 --workload $w > "$R/$O/prof_$w.log" 2>&1 )
   echo "prof $w ok"
+  if [ "$w" = c2 ] || [ "$w" = c3 ]; then
+    # cold-MALL twin: the 256 MiB Infinity Cache flushed (640 MiB fill)
+    # before every timed step; the fill kernel appears in the stats beside the search's
+    ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$O/prof_cold_$w" -o run \
+        --output-format csv -- python3 "$R/bench.py" --no-cpu --no-sweep --inflight 1 --mall-flush --steps 200 --warmup 20 \
+        --workload $w > "$R/$O/prof_cold_$w.log" 2>&1 )
+    echo "prof cold $w ok"
+  fi
   i=0
   for grp in FETCH_SIZE WRITE_SIZE; do
     i=$((i+1))

@@ -25,6 +25,7 @@ FAMILIES = {
     "prep": ("bb::prep_kernel", "bb::prep2_kernel"),
     "finalize": ("bb::finalize1_kernel", "bb::finalize_kernel"),
     "rerank": ("bb::rerank_kernel",),
+    "pack": ("bb::compact_kernel",),
 }
 ANCHOR = {"f32": ("bb::select_list_kernel", "bb::select_kernel", "bb::scan3_kernel"), "c3": ("bb::finalize1_kernel",),
           "c4": ("bb::finalize_kernel", "bb::finalize1_kernel"), "c5": ("bb::finalize_kernel", "bb::finalize1_kernel")}
