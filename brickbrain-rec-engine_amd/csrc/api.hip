@@ -1557,8 +1557,10 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     // per side, serial 0.126 vs 0.121 ms, r04p); BB_DUAL=1 forces the dual list scan.
     static const int dual_sel = ab_env("BB_DUAL") ? atoi(ab_env("BB_DUAL")) : -1;
     static const int sel_wave_env0 = ab_env("BB_SELECT_WAVE") ? atoi(ab_env("BB_SELECT_WAVE")) : -1;
+    // (a packed constraint-first search's scans are a few tiles each: one launch for both
+    // sides, serial 74 -> 69 us at configs[2], r06i)
     const bool dual = dual_sel != 0 && q->mode == BB_MODE_HYBRID && sides == 2 &&
-                      ((s16_c && s16_f) || (list_c && list_f && dual_sel == 1)) &&
+                      ((s16_c && s16_f) || (list_c && list_f && (dual_sel == 1 || x->shadow))) &&
                       !stream &&
                       n_slabs == 1 && scan4_used(BF16, bpad) && scan4_dual_supported((int)x->Dpad_b / 8, (int)x->Rpad_b / 8) &&
                       std::min<int64_t>(slab, x->n) <= 32768 && K_int <= 256 && sel_wave_env0 != 0 && bc > 256;
