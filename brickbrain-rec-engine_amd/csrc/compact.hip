@@ -177,6 +177,18 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
   const int b = gq * 4 + wave;
   if (b >= a.B) return;  // (per wave: no block barrier below)
   uint32_t* rb = rowbits[wave];
+  // the exclusion row's words, all in flight at once and before the rank-0 lookups (a loop
+  // loading one word per step waited a memory round trip per step: ~13 at configs[2])
+  constexpr int kEx = kCompactMaxWords / 64;
+  uint32_t exw[kEx];
+  if (a.c_excl1) {
+    const uint32_t* ex = a.excl + (int64_t)b * a.excl_ld;
+#pragma unroll
+    for (int j = 0; j < kEx; ++j) {
+      const int w = lane + 64 * j;
+      exw[j] = w < nw ? ex[w] : 0u;
+    }
+  }
   auto wave_sync = []() __attribute__((always_inline)) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -203,9 +215,11 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
   if (a.c_excl1) {  // the query's exclusions (rated items), re-indexed to slots
     for (int w = lane; w < a.xnw; w += 64) rb[w] = 0u;
     wave_sync();
-    const uint32_t* ex = a.excl + (int64_t)b * a.excl_ld;
-    for (int w = lane; w < nw; w += 64) {
-      uint32_t hit = mw[w] & ex[w];
+#pragma unroll
+    for (int j = 0; j < kEx; ++j) {
+      const int w = lane + 64 * j;
+      if (w >= nw) continue;
+      uint32_t hit = mw[w] & exw[j];
       while (hit) {
         const int bit = __builtin_ctz(hit);
         hit &= hit - 1u;
