@@ -942,7 +942,7 @@ int compact_search(bb_index* x, const bb_query* q, bb_result* res, hipStream_t s
   a.ch_items_b = need_content ? x->Dpad_b / 8 : 0;
   a.ch_cf = need_cf ? x->Rpad / 4 : 0;
   a.ch_cf_b = need_cf ? x->Rpad_b / 8 : 0;
-  a.n_copy_wg = (int32_t)((a.cap_pos * (a.ch_items + a.ch_cf) + cap * (a.ch_items_b + a.ch_cf_b) + 255) / 256);
+  a.n_copy_wg = (int32_t)((a.cap_pos * (a.ch_items + a.ch_cf) + cap * (a.ch_items_b + a.ch_cf_b) + 1023) / 1024);
   a.idmap = (uint32_t*)c->idmap.p;
   const bool per_query = liked || (need_cf && d_excl);
   a.B = per_query ? B : 0;
@@ -1536,7 +1536,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         }
       }
       if (prep_f) cj.prep_f = pa_f;
-      cj.n_excl_wg = (cj.B + 3) / 4;
+      cj.n_query_wg = (std::max(cj.B, cj.prep_c.Bpad) + 3) / 4;
       x->cjob_set = false;
       if ((rc = timed(x, K_PACK, s, [&] { return launch_compact(cj, s); }))) return rc;
     } else if (prep_c && prep_f) {

@@ -484,7 +484,7 @@ struct CompactArgs {
   int32_t cnw;               // cap / 32 (words of the packed present bitsets)
   int32_t xnw;               // words per row of the packed exclusions (the shadow's ceil(count / 32))
   int32_t n_word_wg;         // cap / 32 workgroups: id map + present words
-  int32_t n_copy_wg;         // workgroups of the row copies (one 16-B piece per thread)
+  int32_t n_copy_wg;         // workgroups of the row copies (four 16-B pieces per thread)
   int32_t ch_items, ch_items_b, ch_cf, ch_cf_b;  // 16-B pieces per row of each copy (0: absent)
   uint32_t* idmap;           // [cap] global id per position (0xFFFFFFFF: padding)
   float* c_items;
@@ -494,7 +494,7 @@ struct CompactArgs {
   uint16_t* c_cf_bf;
   uint32_t* c_cf_present;
   int32_t B;                 // query rows with exclusions
-  int32_t n_excl_wg;         // exclusion workgroups (4 rows each): ceil(B / 4), 0 without exclusions
+  int32_t n_query_wg;        // query workgroups (4 rows each): content prep + exclusions of their rows
   const int64_t* q_items;    // [B] liked sets (global ids) — the rank-0 lookups
   const uint64_t* r0key;     // [n + 1] rank-0 key of each item's own row (the unmasked arg-max); [n]: a zero row's
   uint32_t* c_excl0;         // [B][xnw] content exclusion: the rank-0 item's position, or null

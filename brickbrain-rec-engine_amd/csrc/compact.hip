@@ -24,21 +24,25 @@
 // items, so a per-lane top-5 list of one tile never overflows: when the top-K is a large
 // share of the allowed rows (configs[2]: 101 of ~440), dense packing overflowed most lists
 // and the list select rescored most rows (48 us, r06d).
-//   exclusion workgroups four query rows each, one wave per row: the content exclusion of the
-//                        liked set's rank-0 item (the arg-max of the UNMASKED ranking, :217 —
-//                        known per item from the rank-0 table, so the packed search drops it as
-//                        the full one does) and the query's CF exclusions (rated items,
-//                        :441-451) re-indexed to slots
-//   prep workgroups      four query rows of one side each (no mask prefix): prep_kernel's body
-//                        (prep_body.h — the liked set's stored row gathered by id from the FULL
-//                        index, the CF user row; the f16 operand in the scan's lane order, the
-//                        f32 row and bound), so the packed search launches no prep
+//   query workgroups     four query rows each, one wave per row: the content-side prep
+//                        (prep_kernel's body, prep_body.h — the liked set's stored row gathered
+//                        by id from the FULL index; the f16 operand in the scan's lane order,
+//                        the f32 row and bound), then the content exclusion of the liked set's
+//                        rank-0 item (the arg-max of the UNMASKED ranking, :217 — known per item
+//                        from the rank-0 table, so the packed search drops it as the full one
+//                        does) and the query's CF exclusions (rated items, :441-451) re-indexed
+//                        to slots
+//   CF prep workgroups   four CF user rows each (no mask prefix), prep_kernel's body — so the
+//                        packed search launches no prep of its own.  (One workgroup per CU-slot
+//                        round: 136 VGPRs hold a CU to three workgroups, so the roles are packed
+//                        into as few workgroups as their latency chains allow.)
 #include "common.h"
 #include "prep_body.h"
 
 namespace bb {
 
 constexpr int kCompactThreads = 256;
+constexpr int kCompactPieces = 4;  // 16-B row pieces per copy thread
 
 // p-th set bit of w (0-based; p < popcount(w))
 __device__ __forceinline__ int select_bit(uint32_t w, int p) {
@@ -54,16 +58,17 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nw = a.nw;
   const int g = blockIdx.x;
-  // ---- query prep workgroups (no mask prefix needed): four rows of one side each, one wave
-  // per row — prep_kernel's body (prep_body.h), so the packed search launches no prep ----
-  {
-    const int g0 = a.n_word_wg + a.n_copy_wg + a.n_excl_wg, nc = a.prep_c.Bpad / 4, nf = a.prep_f.Bpad / 4;
-    if (g >= g0) {
-      if (g < g0 + nc) prep_rows(a.prep_c, g - g0);
-      else if (g < g0 + nc + nf) prep_rows(a.prep_f, g - g0 - nc);
-      return;
-    }
+  const int gq0 = a.n_word_wg + a.n_copy_wg;  // first query workgroup
+  // ---- CF prep workgroups (no mask prefix needed): four rows each, one wave per row —
+  // prep_kernel's body (prep_body.h), so the packed search launches no prep ----
+  if (g >= gq0 + a.n_query_wg) {
+    prep_rows(a.prep_f, g - gq0 - a.n_query_wg);
+    return;
   }
+  // query workgroups: the content prep of their four rows (no prefix needed for it), then the
+  // same rows' exclusions (which need it).  Prep first: its loads are the longest chain.
+  if (g >= gq0 && a.prep_c.Bpad) prep_rows(a.prep_c, g - gq0);
+  if (g >= gq0 && !a.B) return;
   // ---- mask words (bits past n cleared) and their exclusive popcount prefix ----
   constexpr int kWpt = kCompactMaxWords / kCompactThreads;
   uint32_t cnt[kWpt];
@@ -132,48 +137,57 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
     return;
   }
   if (g < a.n_word_wg + a.n_copy_wg) {
-    // ---- rows: one 16-B piece per thread over [allowed positions] x [the f32 content and CF
-    // pieces of a row] then [every slot] x [the f16 pieces the scans read] (zeros for the
-    // padding slots; the f32 rows of padding slots are never read: nothing there is present)
-    const int64_t i = (int64_t)(g - a.n_word_wg) * kCompactThreads + tid;
+    // ---- rows: kCompactPieces 16-B pieces per thread (all loads before any store) over
+    // [allowed positions] x [the f32 content and CF pieces of a row] then [every slot] x [the
+    // f16 pieces the scans read] (zeros for the padding slots; the f32 rows of padding slots are
+    // never read: nothing there is present) ----
     const int per32 = a.ch_items + a.ch_cf, per16 = a.ch_items_b + a.ch_cf_b;
     const int64_t n32 = (int64_t)E * per32;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    uint4* dst;
-    if (i < n32) {
-      const int p = (int)(i / per32);
-      int c = (int)(i - (int64_t)p * per32);
-      const int64_t item = item_of(p), sl = (int64_t)p * S;
-      if (c < a.ch_items) {
-        v = ((const uint4*)(a.items + item * a.ld))[c];
-        dst = (uint4*)(a.c_items + sl * a.ld) + c;
+    const int64_t total_pieces = n32 + (int64_t)a.cap * per16;
+    uint4 v[kCompactPieces];
+    uint4* dst[kCompactPieces];
+#pragma unroll
+    for (int u = 0; u < kCompactPieces; ++u) {
+      const int64_t i = ((int64_t)(g - a.n_word_wg) * kCompactPieces + u) * kCompactThreads + tid;
+      v[u] = make_uint4(0u, 0u, 0u, 0u);
+      dst[u] = nullptr;
+      if (i >= total_pieces) continue;
+      if (i < n32) {
+        const int p = (int)(i / per32);
+        int c = (int)(i - (int64_t)p * per32);
+        const int64_t item = item_of(p), sl = (int64_t)p * S;
+        if (c < a.ch_items) {
+          v[u] = ((const uint4*)(a.items + item * a.ld))[c];
+          dst[u] = (uint4*)(a.c_items + sl * a.ld) + c;
+        } else {
+          c -= a.ch_items;
+          v[u] = ((const uint4*)(a.cf + item * a.ldc))[c];
+          dst[u] = (uint4*)(a.c_cf + sl * a.ldc) + c;
+        }
       } else {
-        c -= a.ch_items;
-        v = ((const uint4*)(a.cf + item * a.ldc))[c];
-        dst = (uint4*)(a.c_cf + sl * a.ldc) + c;
-      }
-    } else {
-      const int64_t j = i - n32;
-      const int sl = (int)(j / per16);
-      if (sl >= a.cap) return;
-      int c = (int)(j - (int64_t)sl * per16);
-      const int64_t item = sl % S ? -1 : item_of(sl / S);
-      const int64_t it = item >= 0 ? item : 0;
-      if (c < a.ch_items_b) {
-        if (item >= 0) v = ((const uint4*)(a.items_bf + it * a.ld_b))[c];
-        dst = (uint4*)(a.c_items_bf + (int64_t)sl * a.ld_b) + c;
-      } else {
-        c -= a.ch_items_b;
-        if (item >= 0) v = ((const uint4*)(a.cf_bf + it * a.ldc_b))[c];
-        dst = (uint4*)(a.c_cf_bf + (int64_t)sl * a.ldc_b) + c;
+        const int64_t j = i - n32;
+        const int sl = (int)(j / per16);
+        int c = (int)(j - (int64_t)sl * per16);
+        const int64_t item = sl % S ? -1 : item_of(sl / S);
+        const int64_t it = item >= 0 ? item : 0;
+        if (c < a.ch_items_b) {
+          if (item >= 0) v[u] = ((const uint4*)(a.items_bf + it * a.ld_b))[c];
+          dst[u] = (uint4*)(a.c_items_bf + (int64_t)sl * a.ld_b) + c;
+        } else {
+          c -= a.ch_items_b;
+          if (item >= 0) v[u] = ((const uint4*)(a.cf_bf + it * a.ldc_b))[c];
+          dst[u] = (uint4*)(a.c_cf_bf + (int64_t)sl * a.ldc_b) + c;
+        }
       }
     }
-    *dst = v;
+#pragma unroll
+    for (int u = 0; u < kCompactPieces; ++u)
+      if (dst[u]) *dst[u] = v[u];
     return;
   }
 
   // ---- exclusion rows [4q, 4q + 4), one wave each ----
-  const int gq = g - a.n_word_wg - a.n_copy_wg;
+  const int gq = g - gq0;
   const int b = gq * 4 + wave;
   if (b >= a.B) return;  // (per wave: no block barrier below)
   uint32_t* rb = rowbits[wave];
@@ -238,7 +252,8 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
   if (a.nw <= 0 || a.nw > kCompactMaxWords || a.cap <= 0 || a.cap % 32 || a.cnw * 32 != a.cap ||
       a.cap > kCompactMaxSlots || a.xnw <= 0 || a.xnw > a.cnw || a.n_word_wg != a.cnw || a.B < 0 || per <= 0 ||
       a.stride < 1 || a.cap_pos * a.stride != a.cap ||
-      (int64_t)a.n_copy_wg * kCompactThreads < (int64_t)a.cap_pos * (a.ch_items + a.ch_cf) + (int64_t)a.cap * (a.ch_items_b + a.ch_cf_b) ||
+      (int64_t)a.n_copy_wg * kCompactThreads * kCompactPieces <
+          (int64_t)a.cap_pos * (a.ch_items + a.ch_cf) + (int64_t)a.cap * (a.ch_items_b + a.ch_cf_b) ||
       (a.items && (!a.items_bf || !a.c_items || !a.c_items_bf || !a.c_present || a.ld % 4 || a.ld_b % 8 ||
                    a.ch_items != a.ld / 4 || a.ch_items_b != a.ld_b / 8)) ||
       (!a.items && (a.ch_items || a.ch_items_b)) ||
@@ -246,10 +261,11 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
                 a.ch_cf != a.ldc / 4 || a.ch_cf_b != a.ldc_b / 8)) ||
       (!a.cf && (a.ch_cf || a.ch_cf_b)) ||
       (a.c_excl0 && (!a.q_items || !a.r0key)) || (a.c_excl1 && (!a.excl || a.excl_ld < a.nw)) ||
-      a.n_excl_wg * 4 < a.B || (a.B && !a.c_excl0 && !a.c_excl1) || a.prep_c.Bpad % 4 || a.prep_f.Bpad % 4)
+      a.n_query_wg * 4 < a.B || a.n_query_wg * 4 < a.prep_c.Bpad || (a.B && !a.c_excl0 && !a.c_excl1) ||
+      a.prep_c.Bpad % 4 || a.prep_f.Bpad % 4)
     return hipErrorInvalidValue;
-  bb_launch(compact_kernel, dim3(a.n_word_wg + a.n_copy_wg + a.n_excl_wg + (a.prep_c.Bpad + a.prep_f.Bpad) / 4),
-            dim3(kCompactThreads), 0, s, a);
+  bb_launch(compact_kernel, dim3(a.n_word_wg + a.n_copy_wg + a.n_query_wg + a.prep_f.Bpad / 4), dim3(kCompactThreads), 0,
+            s, a);
   return hipGetLastError();
 }
 
