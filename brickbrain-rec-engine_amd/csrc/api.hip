@@ -1536,7 +1536,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         }
       }
       if (prep_f) cj.prep_f = pa_f;
-      cj.n_query_wg = (std::max(cj.B, cj.prep_c.Bpad) + 3) / 4;
+      cj.n_query_wg = (cj.B + 3) / 4;
       x->cjob_set = false;
       if ((rc = timed(x, K_PACK, s, [&] { return launch_compact(cj, s); }))) return rc;
     } else if (prep_c && prep_f) {

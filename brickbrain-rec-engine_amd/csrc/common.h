@@ -494,7 +494,7 @@ struct CompactArgs {
   uint16_t* c_cf_bf;
   uint32_t* c_cf_present;
   int32_t B;                 // query rows with exclusions
-  int32_t n_query_wg;        // query workgroups (4 rows each): content prep + exclusions of their rows
+  int32_t n_query_wg;        // exclusion workgroups (4 rows each): ceil(B / 4), 0 without exclusions
   const int64_t* q_items;    // [B] liked sets (global ids) — the rank-0 lookups
   const uint64_t* r0key;     // [n + 1] rank-0 key of each item's own row (the unmasked arg-max); [n]: a zero row's
   uint32_t* c_excl0;         // [B][xnw] content exclusion: the rank-0 item's position, or null

@@ -24,18 +24,17 @@
 // items, so a per-lane top-5 list of one tile never overflows: when the top-K is a large
 // share of the allowed rows (configs[2]: 101 of ~440), dense packing overflowed most lists
 // and the list select rescored most rows (48 us, r06d).
-//   query workgroups     four query rows each, one wave per row: the content-side prep
-//                        (prep_kernel's body, prep_body.h — the liked set's stored row gathered
-//                        by id from the FULL index; the f16 operand in the scan's lane order,
-//                        the f32 row and bound), then the content exclusion of the liked set's
-//                        rank-0 item (the arg-max of the UNMASKED ranking, :217 — known per item
-//                        from the rank-0 table, so the packed search drops it as the full one
-//                        does) and the query's CF exclusions (rated items, :441-451) re-indexed
-//                        to slots
-//   CF prep workgroups   four CF user rows each (no mask prefix), prep_kernel's body — so the
-//                        packed search launches no prep of its own.  (One workgroup per CU-slot
-//                        round: 136 VGPRs hold a CU to three workgroups, so the roles are packed
-//                        into as few workgroups as their latency chains allow.)
+//   exclusion workgroups four query rows each, one wave per row: the content exclusion of the
+//                        liked set's rank-0 item (the arg-max of the UNMASKED ranking, :217 —
+//                        known per item from the rank-0 table, so the packed search drops it as
+//                        the full one does) and the query's CF exclusions (rated items,
+//                        :441-451) re-indexed to slots
+//   prep workgroups      four query rows of one side each (no mask prefix): prep_kernel's body
+//                        (prep_body.h — the liked set's stored row gathered by id from the FULL
+//                        index, the CF user row; the f16 operand in the scan's lane order, the
+//                        f32 row and bound), so the packed search launches no prep
+// Short, independent latency chains in one occupancy round: the content prep and the
+// exclusions in one workgroup made the launch 11.5 -> 13.2 us (r06o).
 #include "common.h"
 #include "prep_body.h"
 
@@ -50,7 +49,8 @@ __device__ __forceinline__ int select_bit(uint32_t w, int p) {
   return __builtin_ctz(w);
 }
 
-__global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a) {
+// (four workgroups per CU: 128 VGPRs — every role in one round at configs[2])
+__global__ __launch_bounds__(kCompactThreads) __attribute__((amdgpu_waves_per_eu(4))) void compact_kernel(CompactArgs a) {
   __shared__ uint32_t mw[kCompactMaxWords];
   __shared__ uint32_t pre[kCompactMaxWords + 1];
   __shared__ uint32_t rowbits[kCompactThreads / 64][kCompactMaxSlots / 32];  // exclusion rows: one per wave
@@ -58,17 +58,17 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nw = a.nw;
   const int g = blockIdx.x;
-  const int gq0 = a.n_word_wg + a.n_copy_wg;  // first query workgroup
-  // ---- CF prep workgroups (no mask prefix needed): four rows each, one wave per row —
-  // prep_kernel's body (prep_body.h), so the packed search launches no prep ----
-  if (g >= gq0 + a.n_query_wg) {
-    prep_rows(a.prep_f, g - gq0 - a.n_query_wg);
-    return;
+  const int gq0 = a.n_word_wg + a.n_copy_wg;  // first exclusion workgroup
+  // ---- prep workgroups (no mask prefix needed): four rows of one side each, one wave per row
+  // — prep_kernel's body (prep_body.h), so the packed search launches no prep ----
+  {
+    const int g0 = gq0 + a.n_query_wg, nc = a.prep_c.Bpad / 4;
+    if (g >= g0) {
+      if (g < g0 + nc) prep_rows(a.prep_c, g - g0);
+      else prep_rows(a.prep_f, g - g0 - nc);
+      return;
+    }
   }
-  // query workgroups: the content prep of their four rows (no prefix needed for it), then the
-  // same rows' exclusions (which need it).  Prep first: its loads are the longest chain.
-  if (g >= gq0 && a.prep_c.Bpad) prep_rows(a.prep_c, g - gq0);
-  if (g >= gq0 && !a.B) return;
   // ---- mask words (bits past n cleared) and their exclusive popcount prefix ----
   constexpr int kWpt = kCompactMaxWords / kCompactThreads;
   uint32_t cnt[kWpt];
@@ -186,6 +186,7 @@ __global__ __launch_bounds__(kCompactThreads) void compact_kernel(CompactArgs a)
     return;
   }
 
+  if (g >= gq0 && !a.B) return;  // (no exclusion rows)
   // ---- exclusion rows [4q, 4q + 4), one wave each ----
   const int gq = g - gq0;
   const int b = gq * 4 + wave;
@@ -261,11 +262,11 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
                 a.ch_cf != a.ldc / 4 || a.ch_cf_b != a.ldc_b / 8)) ||
       (!a.cf && (a.ch_cf || a.ch_cf_b)) ||
       (a.c_excl0 && (!a.q_items || !a.r0key)) || (a.c_excl1 && (!a.excl || a.excl_ld < a.nw)) ||
-      a.n_query_wg * 4 < a.B || a.n_query_wg * 4 < a.prep_c.Bpad || (a.B && !a.c_excl0 && !a.c_excl1) ||
+      a.n_query_wg * 4 < a.B || (a.B && !a.c_excl0 && !a.c_excl1) ||
       a.prep_c.Bpad % 4 || a.prep_f.Bpad % 4)
     return hipErrorInvalidValue;
-  bb_launch(compact_kernel, dim3(a.n_word_wg + a.n_copy_wg + a.n_query_wg + a.prep_f.Bpad / 4), dim3(kCompactThreads), 0,
-            s, a);
+  bb_launch(compact_kernel, dim3(a.n_word_wg + a.n_copy_wg + a.n_query_wg + (a.prep_c.Bpad + a.prep_f.Bpad) / 4),
+            dim3(kCompactThreads), 0, s, a);
   return hipGetLastError();
 }
 
