@@ -1568,7 +1568,6 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     GemmArgs ga_dual0{};
     SelectArgs sa_dual0{};
     int final_pp = 0;
-    bool hyb_fused = false;  // the packed hybrid's fused select + blend wrote the results
     for (int side = 0; side < sides; ++side) {
       const bool cf_side = (q->mode == BB_MODE_CF) || (q->mode == BB_MODE_HYBRID && side == 1);
       const bool side_drop = drop && side == 0;
@@ -1869,31 +1868,6 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
             BB_HIP(hipMemsetAsync(x->trace.p, 0, (size_t)bc * 128, s));
             (both ? sa_dual0 : sa).trace = (uint64_t*)x->trace.p;
           }
-          // a packed hybrid search (no rank-0 drop): both list selects and the blend in one
-          // workgroup per row (select_list_hybrid_kernel); BB_HYB_FUSED=0 (A/B runs) keeps the
-          // dual select + finalize1
-          static const int hyb_fused_env = ab_env("BB_HYB_FUSED") ? atoi(ab_env("BB_HYB_FUSED")) : -1;
-          if (both && x->shadow && !drop && !out_keys && hyb_fused_env != 0 && K_int <= kHybFusedK) {
-            FinalizeArgs fh{};
-            fh.P = 1;
-            fh.sides = 2;
-            fh.B = (int)Bc;
-            fh.K_int = K_int;
-            fh.drop_rank0 = 0;
-            fh.k = q->k;
-            fh.k_side = q->k_side > 0 ? q->k_side : 2 * q->k;
-            fh.hybrid = 1;
-            fh.w_content = q->w_content;
-            fh.w_cf = q->w_cf;
-            fh.scores = o_sc + (size_t)b0 * q->k;
-            fh.ids = o_id + (size_t)b0 * q->k;
-            fh.counts = o_cnt ? o_cnt + b0 : nullptr;
-            fh.n_rows = bc;
-            fh.idmap = (const uint32_t*)x->idmap.p;
-            if ((rc = timed(x, K_SELECT, s, [&] { return launch_select_list_hybrid(sa_dual0, sa, fh, bc, s); }))) return rc;
-            hyb_fused = true;
-            continue;
-          }
           if ((rc = timed(x, K_SELECT, s, [&] { return launch_select_list(both ? sa_dual0 : sa, both ? &sa : nullptr, bc, s); })))
             return rc;
           if (ls_trace) {
@@ -2028,7 +2002,7 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         final_pp = pp;
       }
     }
-    if (fuse_final || hyb_fused) continue;
+    if (fuse_final) continue;
     const uint64_t* fin_keys = keys + (size_t)final_pp * sides * side_keys;
     if (out_keys) {  // key lists out: device buffers, or host buffers (copied, synchronised below)
       const hipMemcpyKind kind = res->where == BB_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;

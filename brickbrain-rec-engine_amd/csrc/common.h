@@ -387,9 +387,6 @@ struct SelectArgs {
   // constraint-first search (compact.hip): keys carry positions in the packed rows; the final
   // ids written are idmap[position] (global ids), null = keys carry global ids
   const uint32_t* idmap;
-  // list select: this row's key list goes here (e.g. LDS of a fused kernel) instead of
-  // keys_out + row·K
-  uint64_t* keys_row;
 };
 constexpr int kRrCap = 512;
 constexpr int kRrR0Cap = 64;
@@ -550,11 +547,6 @@ hipError_t launch_select_rr_wave_dual(const SelectArgs& a0, const SelectArgs& a1
 // exact top-K of a kScanList scan (lists set, rr_* operands, one slab): one workgroup per row;
 // a1 != null: both sides of a hybrid search in one launch
 hipError_t launch_select_list(const SelectArgs& a0, const SelectArgs* a1, int B, hipStream_t s);
-// both hybrid sides' list selects and the union blend (finalize1's body) in one workgroup per
-// row, the side lists kept in LDS: packed searches (no rank-0 drop), K_int <= kHybFusedK
-constexpr int kHybFusedK = 128;
-hipError_t launch_select_list_hybrid(const SelectArgs& a0, const SelectArgs& a1, const FinalizeArgs& fa, int B,
-                                     hipStream_t s);
 hipError_t launch_cand_select(const CandSelectArgs& a, int B, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 // streaming bound of each query row from a kScanPilot scan: the K-th largest of its

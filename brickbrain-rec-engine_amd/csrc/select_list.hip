@@ -26,7 +26,6 @@
 // Buffer overflow (masses of near-duplicates, all-equal scores): an exact running top-K over
 // every eligible item of the row (slow, never taken on distinct data; tests drive it).
 #include "common.h"
-#include "finalize_body.h"
 #include "list_epi.h"
 #include "qnorm.h"
 #include "select_util.h"
@@ -508,7 +507,7 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
         }
         if (a.out_counts && tid == 0) a.out_counts[row] = c;
       } else {
-        uint64_t* out = a.keys_row ? a.keys_row : a.keys_out + (size_t)row * K;
+        uint64_t* out = a.keys_out + (size_t)row * K;
 #pragma unroll
         for (int e = 0; e < E; ++e)
           if (tid + e * kSelectThreads < Mc && rk[e] < (uint32_t)K) out[rk[e]] = mk[e];
@@ -585,7 +584,7 @@ __device__ __forceinline__ void select_list_body(const SelectArgs& a, int row) {
     if (a.out_counts && tid == 0) a.out_counts[row] = c;
     return;
   }
-  uint64_t* out = a.keys_row ? a.keys_row : a.keys_out + (size_t)row * K;
+  uint64_t* out = a.keys_out + (size_t)row * K;
   for (int i = tid; i < K; i += kSelectThreads) out[i] = sel[i];
 }
 
@@ -615,35 +614,6 @@ static bool list_args_ok(const SelectArgs& a) {
          (a.l_tiles + a.l_chunks - 1) / a.l_chunks <= 2047 && !(a.slab_start & 31) && !a.carry_in &&
          (!a.max_inout || a.r0lists) && (a.out_scores ? (a.out_ids && a.k_final > 0 && a.k_final <= kMaxKInt)
                                                       : a.keys_out != nullptr);
-}
-
-// Both sides of a packed hybrid search and their blend in one workgroup per row: the content
-// list select, the CF list select, then finalize1's union blend over the two lists held in
-// LDS — one launch and no key round trip through global memory where the dual select +
-// finalize1 took two launches (the finalize spent 5 of its 11 us loading the lists, r06k).
-__global__ __launch_bounds__(kSelectThreads) __attribute__((amdgpu_waves_per_eu(4))) void select_list_hybrid_kernel(
-    SelectArgs a0, SelectArgs a1, FinalizeArgs fa, int B) {
-  __shared__ uint64_t hk[2][kHybFusedK];
-  const int row = xcd_row(blockIdx.x, B);
-  SelectArgs s0 = a0;
-  s0.keys_row = hk[0];
-  select_list_body(s0, row);
-  __syncthreads();
-  SelectArgs s1 = a1;
-  s1.keys_row = hk[1];
-  select_list_body(s1, row);
-  __syncthreads();
-  finalize1_body<kHybFusedK>(fa, row, hk[0], hk[1], 0ull);
-}
-
-hipError_t launch_select_list_hybrid(const SelectArgs& a0, const SelectArgs& a1, const FinalizeArgs& fa, int B,
-                                     hipStream_t s) {
-  if (B <= 0 || !list_args_ok(a0) || !list_args_ok(a1) || a0.out_scores || a1.out_scores || a0.max_inout ||
-      a0.K > kHybFusedK || a1.K > kHybFusedK || fa.K_int != a0.K || fa.K_int != a1.K || fa.sides != 2 || !fa.hybrid ||
-      fa.drop_rank0 || fa.P != 1 || !fa.scores || !fa.ids || fa.n_rows != B || fa.k <= 0 || fa.k_side <= 0)
-    return hipErrorInvalidValue;
-  bb_launch(select_list_hybrid_kernel, dim3(B), dim3(kSelectThreads), 0, s, a0, a1, fa, B);
-  return hipGetLastError();
 }
 
 hipError_t launch_select_list(const SelectArgs& a0, const SelectArgs* a1, int B, hipStream_t s) {
