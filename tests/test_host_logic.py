@@ -139,3 +139,46 @@ def test_blend_sure_is_sound_and_tight():
                 assert i in got and abs(got[i] - h) < 1e-12
         if trial % 2 == 0:
             assert len(sure) >= k - 2
+
+
+def test_constraint_first_equivalence():
+    """DESIGN §3a'' (compact.hip), the argument on the CPU oracle: searching only the rows the
+    mask allows — packed in ascending id order at slot p·stride, the liked set's rank-0 item
+    (the arg-max of the UNMASKED ranking, recommendation_system.py:217, from a per-item table)
+    excluded when it is allowed, ties by slot — gives exactly get_similar_sets' masked list,
+    and the CF and hybrid lists too.  Duplicate rows make rank 0 another id (and an allowed
+    one); masks from 0 to all rows; strides 1, 2 and 4."""
+    from oracle import restatement as R
+    rng = np.random.default_rng(11)
+    n, d, r, k = 600, 16, 4, 7
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    x[[50, 90, 400]] = x[20]                 # rank 0 of 50 / 90 / 400 is 20 (lowest id of the twins)
+    f = (0.1 * rng.standard_normal((n, r))).astype(np.float32)
+    # the oracle's own scores, row by row as get_similar_sets computes them: the argument is
+    # about which rows are searched, not about arithmetic
+    sims = np.stack([R.cosine_scores(x[i:i + 1], x)[0] for i in range(n)])
+    r0_table = np.array([R.rank0(sims[i]) for i in range(n)])      # the upload-time table
+    for density in (0.0, 0.02, 0.3, 1.0):
+        mask = rng.random(n) < density
+        mask[[20, 50]] = density > 0
+        allowed = np.flatnonzero(mask)
+        for stride in (1, 2, 4):
+            slots = np.full(max(len(allowed), 1) * stride, -1, np.int64)
+            slots[::stride][:len(allowed)] = allowed                 # slot -> id (idmap)
+            real = slots >= 0
+            for liked in (20, 50, 90, 7, 599):
+                want_i, want_s = R.similar_sets(x, liked, k, mask)
+                s = np.where(real, sims[liked][np.maximum(slots, 0)], -np.inf)
+                ok = real.copy()
+                r0 = r0_table[liked]
+                if mask[r0]:
+                    ok[np.flatnonzero(slots == r0)] = False          # the content exclusion bit
+                got_slot, got_s = R.topk_indices(s, k, ok)
+                assert list(slots[got_slot]) == list(want_i), (density, stride, liked)
+                assert np.array_equal(got_s, want_s)
+            u = (0.1 * rng.standard_normal(r)).astype(np.float32)
+            rated = rng.random(n) < 0.05
+            want_i, _ = R.cf_topk(u, f, k, mask, rated)
+            fs = np.where(real, (f @ u)[np.maximum(slots, 0)], -np.inf)
+            got_slot, _ = R.topk_indices(fs, k, real & ~rated[np.maximum(slots, 0)])
+            assert list(slots[got_slot]) == list(want_i)
