@@ -115,7 +115,7 @@ def family_kernels(workload, dtype, B, scan_name):
     if workload == "c3":
         return {"pack": "compact_kernel (constraint-first packing of the allowed rows + both sides' query prep)",
                 "prep": "prep2_kernel", "gemm": scan_name, "select": "select_list_dual_kernel",
-                "finalize": "finalize1_kernel"}
+                "finalize": "finalize1_small_kernel (one wave per row: side lists of <= 64 keys)"}
     return {"prep": "prep_kernel", "gemm": scan_name,
             "select": "select_list_kernel" if dtype == "f32" else "select_kernel", "rerank": "rerank_kernel",
             "finalize": "finalize1_kernel"}
@@ -718,6 +718,7 @@ def main():
             with torch.cuda.stream(lanes[i % len(lanes)][1]):
                 flush.fill_(i & 0xFF)
         lanes[i % len(lanes)][2]()
+    t_issue = time.perf_counter() - t0          # host time to issue the K steps (diagnostic)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -843,6 +844,7 @@ def main():
         "p50_ms": round(float(np.median(lat_ms)), 4),
         "p50_ms_serial": round(float(np.median(lat_serial)), 4),
         "p50_ms_mall_cold": round(float(np.median(cold)), 4),
+        "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -31,7 +31,7 @@ __device__ __forceinline__ uint64_t ord64_of(double d) {
 // up in the other list, and every blended entry finds its output position as its rank
 // under (h desc, id asc) — O(n²) independent comparisons, n <= 2·k_side, no barriers inside.
 // k0 / k1: the side lists (a.K_int keys each, generic pointers: global or LDS).
-template <int KC>
+template <int KC, int NT = kFinThreads>
 __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, const uint64_t* k0, const uint64_t* k1,
                                                uint64_t maxk) {
   __shared__ uint64_t lst[2][KC];
@@ -48,15 +48,19 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   // both side lists into registers first: a barrier waits for every outstanding load, so
   // loads issued after the setup barrier would add a second memory round trip (r04r trace:
   // 5.9 us until the lists were in LDS)
-  constexpr int KR = (KC + kFinThreads - 1) / kFinThreads;
+  constexpr int KR = (KC + NT - 1) / NT;
   uint64_t kv[2][KR];
 #pragma unroll
   for (int side = 0; side < 2; ++side)
 #pragma unroll
     for (int j = 0; j < KR; ++j) {
-      const int i = tid + j * kFinThreads;
+      const int i = tid + j * NT;
       kv[side][j] = side < a.sides && i < a.K_int ? (side ? k1 : k0)[i] : 0ull;
     }
+  if (kProbes && a.trace) {  // probe: the list loads' own latency
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(6);
+  }
   if (tid < 2) nnz[tid] = 0;
   if (tid == 0) n_ent = 0;
   __syncthreads();
@@ -65,18 +69,23 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   for (int side = 0; side < 2; ++side)
 #pragma unroll
     for (int j = 0; j < KR; ++j) {
-      const int i = tid + j * kFinThreads;
+      const int i = tid + j * NT;
       if (side < a.sides && i < a.K_int) {
         lst[side][i] = kv[side][j];
         cnt_local[side] += kv[side][j] != 0ull;
       }
     }
-  for (int side = 0; side < a.sides; ++side)
-    if (cnt_local[side]) atomicAdd(&nnz[side], cnt_local[side]);
+  // (side loops unrolled with constant indices: a loop bounded by a.sides indexed these
+  // arrays dynamically and put them in scratch — a memory round trip per access)
+#pragma unroll
+  for (int side = 0; side < 2; ++side)
+    if (side < a.sides && cnt_local[side]) atomicAdd(&nnz[side], cnt_local[side]);
   __syncthreads();
   stamp(1);
   int start[2] = {0, 0}, c[2] = {0, 0};
-  for (int side = 0; side < a.sides; ++side) {
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    if (side >= a.sides) continue;
     const uint64_t head = lst[side][0];
     if (side == 0 && a.drop_rank0 && maxk && head && head == maxk) start[side] = 1;
     const int target = a.hybrid ? a.k_side : a.k;
@@ -86,11 +95,13 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   float* sc = a.scores + (size_t)q * a.k;
   int64_t* id = a.ids + (size_t)q * a.k;
   if (!a.hybrid || c[0] == 0 || c[1] == 0) {
-    const int side = (!a.hybrid || c[0] > 0) ? 0 : 1;
-    const int n = c[side] < a.k ? c[side] : a.k;
-    for (int i = tid; i < a.k; i += kFinThreads) {
+    const bool s1 = a.hybrid && c[0] == 0;
+    const int cs = s1 ? c[1] : c[0];
+    const uint64_t* L = s1 ? lst[1] + start[1] : lst[0] + start[0];
+    const int n = cs < a.k ? cs : a.k;
+    for (int i = tid; i < a.k; i += NT) {
       if (i < n) {
-        const uint64_t key = lst[side][start[side] + i];
+        const uint64_t key = L[i];
         sc[i] = float_of_ord(ordk_of(key));
         id[i] = out_id(a.idmap, gid_of(key));
       } else {
@@ -110,12 +121,12 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   __shared__ uint32_t tab_g[kTab];   // gid + 1 (0 = empty)
   __shared__ uint16_t tab_j[kTab];
   __shared__ uint8_t used[KC];
-  for (int i = tid; i < kTab; i += kFinThreads) tab_g[i] = 0u;
-  for (int j = tid; j < c[1]; j += kFinThreads) used[j] = 0;
+  for (int i = tid; i < kTab; i += NT) tab_g[i] = 0u;
+  for (int j = tid; j < c[1]; j += NT) used[j] = 0;
   __syncthreads();
   stamp(2);
   auto slot0 = [](uint32_t g) { return (int)((g * 2654435761u) >> 22) & (kTab - 1); };
-  for (int j = tid; j < c[1]; j += kFinThreads) {
+  for (int j = tid; j < c[1]; j += NT) {
     const uint32_t g = gid_of(L1[j]);
     for (int sl = slot0(g);; sl = (sl + 1) & (kTab - 1))
       if (atomicCAS(&tab_g[sl], 0u, g + 1u) == 0u) {
@@ -124,7 +135,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
       }
   }
   __syncthreads();
-  for (int i = tid; i < c[0]; i += kFinThreads) {
+  for (int i = tid; i < c[0]; i += NT) {
     const uint32_t g = gid_of(L0[i]);
     int hit = -1;
     for (int sl = slot0(g);; sl = (sl + 1) & (kTab - 1)) {
@@ -145,7 +156,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   }
   __syncthreads();
   stamp(3);
-  for (int j = tid; j < c[1]; j += kFinThreads) {
+  for (int j = tid; j < c[1]; j += NT) {
     const uint32_t g = gid_of(L1[j]);
     if (!used[j]) {
       const int pos = c[0] + atomicAdd(&n_ent, 1);
@@ -166,7 +177,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   // comparison among them, batched the same way.  The
   // full 96-bit count for every pair, with 32 LDS reads per round, took 9.5 us of the 21 us
   // kernel at configs[2] (r02u trace).
-  for (int e = tid; e < ne; e += kFinThreads) {
+  for (int e = tid; e < ne; e += NT) {
     const uint64_t hk = ek[e];
     const uint32_t g = eg[e], hh = ehi[e];
     int gt = 0, ge = 0, f = 0;
@@ -205,13 +216,17 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
       id[rank] = out_id(a.idmap, g);
     }
   }
-  for (int i = n + tid; i < a.k; i += kFinThreads) {
+  for (int i = n + tid; i < a.k; i += NT) {
     sc[i] = 0.f;
     id[i] = -1;
   }
   if (a.counts && tid == 0) a.counts[q] = n;
   __syncthreads();
   stamp(5);
+  if (kProbes && a.trace) {  // probe: the output stores' completion
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(7);
+  }
 }
 
 

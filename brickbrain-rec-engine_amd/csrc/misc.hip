@@ -194,6 +194,16 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
                            a.drop_rank0 && a.max_keys ? a.max_keys[q] : 0ull);
 }
 
+// Side lists of <= 64 keys (k <= 63: every configs[2]-shaped hybrid): one wave per row, the
+// tables sized to the lists (≈5 KiB of LDS instead of ≈38 KiB), so a CU holds many rows and
+// the barriers are one wave's.
+constexpr int kFinSmallK = 64;
+__global__ __launch_bounds__(64) void finalize1_small_kernel(FinalizeArgs a) {
+  const int q = blockIdx.x;
+  finalize1_body<kFinSmallK, 64>(a, q, a.keys + (size_t)q * a.K_int, a.keys + ((size_t)a.B + q) * a.K_int,
+                                 a.drop_rank0 && a.max_keys ? a.max_keys[q] : 0ull);
+}
+
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(FinalizeArgs a) {
   __shared__ uint64_t buf[kFinMerge];
   __shared__ uint64_t lists[2][kMaxKInt];
@@ -442,7 +452,10 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
   if (a.n_rows > a.B || a.P * a.K_int > kFinMerge || a.K_int > kMaxKInt || a.sides < 1 || a.sides > 2) return hipErrorInvalidValue;
   static const bool legacy = ab_env("BB_FINALIZE_LEGACY") != nullptr;
-  if (a.P == 1 && !legacy)
+  static const bool wide = ab_env("BB_FIN_WIDE") != nullptr;
+  if (a.P == 1 && !legacy && a.K_int <= kFinSmallK && !wide)
+    bb_launch(finalize1_small_kernel, dim3(a.n_rows), dim3(64), 0, s, a);
+  else if (a.P == 1 && !legacy)
     bb_launch(finalize1_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
   else
     bb_launch(finalize_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
