@@ -115,7 +115,7 @@ def family_kernels(workload, dtype, B, scan_name):
     if workload == "c3":
         return {"pack": "compact_kernel (constraint-first packing of the allowed rows + both sides' query prep)",
                 "prep": "prep2_kernel", "gemm": scan_name, "select": "select_list_dual_kernel",
-                "finalize": "finalize1_small_kernel (one wave per row: side lists of <= 64 keys)"}
+                "finalize": "finalize1_mid_kernel (two waves per row: side lists of <= 128 keys)"}
     return {"prep": "prep_kernel", "gemm": scan_name,
             "select": "select_list_kernel" if dtype == "f32" else "select_kernel", "rerank": "rerank_kernel",
             "finalize": "finalize1_kernel"}

@@ -40,11 +40,16 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   __shared__ uint32_t eg[2 * KC];
   __shared__ __attribute__((aligned(16))) uint32_t ehi[2 * KC];  // order image of (float)eh
   __shared__ int nnz[2], n_ent;
+  constexpr int kSamp = 64;  // pruning sample (hybrid ranking, below)
+  __shared__ uint32_t samp[kSamp];
+  __shared__ int n_samp_cf, n_surv;
+  __shared__ uint32_t prune_t;
   const int tid = threadIdx.x;
   auto stamp = [&](int slot) {  // probe-only phase timeline (s_memrealtime, 100 MHz)
     if (a.trace && tid == 0) a.trace[q * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
+  if (a.trace && tid == 0) a.trace[q * 8 + 6] = __builtin_amdgcn_s_memtime();  // probe: shader clock
   // both side lists into registers first: a barrier waits for every outstanding load, so
   // loads issued after the setup barrier would add a second memory round trip (r04r trace:
   // 5.9 us until the lists were in LDS)
@@ -57,12 +62,15 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
       const int i = tid + j * NT;
       kv[side][j] = side < a.sides && i < a.K_int ? (side ? k1 : k0)[i] : 0ull;
     }
-  if (kProbes && a.trace) {  // probe: the list loads' own latency
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp(6);
+  if (a.abl == 1) {
+    if (kv[0][0] == 1ull && kv[1][0] == 1ull) a.scores[0] = 0.f;  // (keeps the loads)
+    return;
   }
   if (tid < 2) nnz[tid] = 0;
-  if (tid == 0) n_ent = 0;
+  if (tid == 0) {
+    n_ent = 0;
+    n_samp_cf = 0;
+  }
   __syncthreads();
   int cnt_local[2] = {0, 0};
 #pragma unroll
@@ -82,6 +90,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
     if (side < a.sides && cnt_local[side]) atomicAdd(&nnz[side], cnt_local[side]);
   __syncthreads();
   stamp(1);
+  if (a.abl == 3) return;  // (A/B probe: stop here)
   int start[2] = {0, 0}, c[2] = {0, 0};
 #pragma unroll
   for (int side = 0; side < 2; ++side) {
@@ -118,13 +127,14 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   const uint64_t* L0 = lst[0] + start[0];
   const uint64_t* L1 = lst[1] + start[1];
   constexpr int kTab = 2 * KC;
-  __shared__ uint32_t tab_g[kTab];   // gid + 1 (0 = empty)
+  __shared__ __attribute__((aligned(16))) uint32_t tab_g[kTab];  // gid + 1 (0 = empty); later the survivors' images
   __shared__ uint16_t tab_j[kTab];
   __shared__ uint8_t used[KC];
   for (int i = tid; i < kTab; i += NT) tab_g[i] = 0u;
   for (int j = tid; j < c[1]; j += NT) used[j] = 0;
   __syncthreads();
   stamp(2);
+  if (a.abl == 4) return;  // (A/B probe: stop here)
   auto slot0 = [](uint32_t g) { return (int)((g * 2654435761u) >> 22) & (kTab - 1); };
   for (int j = tid; j < c[1]; j += NT) {
     const uint32_t g = gid_of(L1[j]);
@@ -156,6 +166,13 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   }
   __syncthreads();
   stamp(3);
+  if (a.abl == 5) return;  // (A/B probe: stop here)
+  // sample S for the pruning bound below: the first content entries (L0 order: the best
+  // content scores, blended), topped up with the best CF-only entries (L1 order) when the
+  // content list is short — at most kSamp together.  (The two side lists of a selective
+  // mask overlap heavily, so few CF-only entries come from the head of L1.)
+  const int c0s = c[0] < kSamp ? c[0] : kSamp;
+  for (int i = tid; i < c0s; i += NT) samp[i] = ehi[i];
   for (int j = tid; j < c[1]; j += NT) {
     const uint32_t g = gid_of(L1[j]);
     if (!used[j]) {
@@ -164,56 +181,89 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
       ek[pos] = ord64_of(eh[pos]);
       ehi[pos] = ord_of((float)eh[pos]);
       eg[pos] = g;
+      if (j < kSamp - c0s) samp[c0s + atomicAdd(&n_samp_cf, 1)] = ehi[pos];
     }
   }
   __syncthreads();
   stamp(4);
+  if (a.abl == 6) return;  // (A/B probe: stop here)
   const int ne = c[0] + n_ent;
   const int n = ne < a.k ? ne : a.k;
-  // output position = rank under (h desc, id asc).  Counted on the order image of the f32
-  // rounding of h first (monotonic in h; 16 entries per round from four ds_read_b128
-  // broadcasts, two 32-bit compares each): entries above are better, below worse.  Only
-  // entries sharing that image with others (ties and near-ties, rare) take the full (h, id)
-  // comparison among them, batched the same way.  The
-  // full 96-bit count for every pair, with 32 LDS reads per round, took 9.5 us of the 21 us
-  // kernel at configs[2] (r02u trace).
-  for (int e = tid; e < ne; e += NT) {
+  // Pruning bound (exact): T = the k-th largest f32 image in the sample S.  At least k
+  // entries reach T, so an entry below it ranks >= k and is dropped; an entry at or above
+  // T has every entry that outranks it at or above T too, so its rank among the survivors
+  // is its rank among all entries.  The O(n²) rank count then runs over the survivors
+  // only (configs[2]: ~200 entries, the count was 9 of the kernel's 16.7 us).
+  const int ns = c0s + n_samp_cf;
+  if (tid < 64) {
+    uint32_t t = 0u;  // fewer than k samples: no bound
+    if (ns >= a.k && tid < ns) {
+      const uint32_t v = samp[tid];
+      int gt = 0, ge = 0;
+      for (int f = 0; f < ns; ++f) {
+        const uint32_t u = samp[f];
+        gt += u > v;
+        ge += u >= v;
+      }
+      t = (gt < a.k && ge >= a.k) ? v : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t = max(t, (uint32_t)__shfl_xor((int)t, o));
+    if (tid == 0) {
+      prune_t = t;
+      n_surv = 0;
+    }
+  }
+  __syncthreads();
+  // survivors, compacted: their images (reusing the hash table's words) and entry indices
+  uint32_t* sv_h = tab_g;
+  uint16_t* sv_e = tab_j;
+  const uint32_t T = prune_t;
+  for (int e = tid; e < ne; e += NT)
+    if (ehi[e] >= T) {
+      const int si = atomicAdd(&n_surv, 1);
+      sv_h[si] = ehi[e];
+      sv_e[si] = (uint16_t)e;
+    }
+  __syncthreads();
+  const int nsv = n_surv;
+  // output position = rank under (h desc, id asc), counted on the order image of the f32
+  // rounding of h first (monotonic in h; 16 survivors per round from four ds_read_b128
+  // broadcasts): entries above are better, below worse.  Only survivors sharing that image
+  // with others (ties and near-ties, rare) take the full (h, id) comparison among them.
+  for (int si = tid; si < nsv; si += NT) {
+    const int e = sv_e[si];
     const uint64_t hk = ek[e];
     const uint32_t g = eg[e], hh = ehi[e];
-    int gt = 0, ge = 0, f = 0;
-    for (; f + 16 <= ne; f += 16) {
+    // the output id (a packed search maps slots through idmap: a global gather) is loaded
+    // before the count, so its latency hides under it instead of following it
+    const int64_t oid = a.abl == 9 ? (int64_t)g : out_id(a.idmap, g);
+    int gt = 0, ge = 0, f = a.abl == 8 ? nsv : 0;
+    const int nsv_c = a.abl == 12 ? (nsv < 16 ? nsv : 16) : nsv;  // (A/B probe: one block)
+    for (; f + 16 <= nsv_c; f += 16) {
       uint32_t kk[16];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) *(uint4*)(kk + 4 * j) = *(const uint4*)(ehi + f + 4 * j);
+      for (int j = 0; j < 4; ++j) *(uint4*)(kk + 4 * j) = *(const uint4*)(sv_h + f + 4 * j);
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         gt += kk[j] > hh;
         ge += kk[j] >= hh;
       }
     }
-    for (; f < ne; ++f) {
-      gt += ehi[f] > hh;
-      ge += ehi[f] >= hh;
+    for (; f < nsv_c; ++f) {
+      gt += sv_h[f] > hh;
+      ge += sv_h[f] >= hh;
     }
-    int rank = gt;
+    int rank = a.abl == 8 ? si : gt;
     if (ge - gt > 1) {
-      for (f = 0; f + 16 <= ne; f += 16) {
-        uint32_t kk[16], gg[16];
-        uint64_t hv[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          kk[j] = ehi[f + j];
-          hv[j] = ek[f + j];
-          gg[j] = eg[f + j];
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) rank += kk[j] == hh && ((hv[j] > hk) || (hv[j] == hk && gg[j] < g));
+      for (int f = 0; f < nsv; ++f) {
+        const int x = sv_e[f];
+        rank += sv_h[f] == hh && ((ek[x] > hk) || (ek[x] == hk && eg[x] < g));
       }
-      for (; f < ne; ++f) rank += ehi[f] == hh && ((ek[f] > hk) || (ek[f] == hk && eg[f] < g));
     }
-    if (rank < a.k) {
+    if (rank < a.k && a.abl != 7) {
       sc[rank] = (float)eh[e];
-      id[rank] = out_id(a.idmap, g);
+      id[rank] = oid;
     }
   }
   for (int i = n + tid; i < a.k; i += NT) {
@@ -223,10 +273,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   if (a.counts && tid == 0) a.counts[q] = n;
   __syncthreads();
   stamp(5);
-  if (kProbes && a.trace) {  // probe: the output stores' completion
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp(7);
-  }
+  if (a.trace && tid == 0) a.trace[q * 8 + 7] = __builtin_amdgcn_s_memtime();
 }
 
 

@@ -23,11 +23,11 @@ FAMILIES = {
     "select": ("bb::select_list_kernel", "bb::select_list_dual_kernel", "bb::select_kernel", "bb::select_rr_wave",
                "bb::cand_select_kernel", "bb::cand_select_wave_kernel", "bb::pilot_bound", "bb::(anonymous namespace)::sq_merge_kernel"),
     "prep": ("bb::prep_kernel", "bb::prep2_kernel"),
-    "finalize": ("bb::finalize1_kernel", "bb::finalize1_small_kernel", "bb::finalize_kernel"),
+    "finalize": ("bb::finalize1_kernel", "bb::finalize1_small_kernel", "bb::finalize1_mid_kernel", "bb::finalize_kernel"),
     "rerank": ("bb::rerank_kernel",),
     "pack": ("bb::compact_kernel",),
 }
-ANCHOR = {"f32": ("bb::select_list_kernel", "bb::select_kernel", "bb::scan3_kernel"), "c3": ("bb::finalize1_small_kernel", "bb::finalize1_kernel"),
+ANCHOR = {"f32": ("bb::select_list_kernel", "bb::select_kernel", "bb::scan3_kernel"), "c3": ("bb::finalize1_mid_kernel", "bb::finalize1_small_kernel", "bb::finalize1_kernel"),
           "c4": ("bb::finalize_kernel", "bb::finalize1_kernel"), "c5": ("bb::finalize_kernel", "bb::finalize1_kernel")}
 
 
