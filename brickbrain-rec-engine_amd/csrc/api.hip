@@ -2037,8 +2037,6 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
     fa.counts = o_cnt ? o_cnt + b0 : nullptr;
     fa.n_rows = bc;
     fa.idmap = x->shadow ? (const uint32_t*)x->idmap.p : nullptr;
-    static const int fin_abl = ab_env("BB_FIN_ABL") ? atoi(ab_env("BB_FIN_ABL")) : 0;
-    fa.abl = fin_abl;
     static const bool fin_trace = kProbes && ab_env("BB_SELECT_TRACE") != nullptr;
     if (fin_trace) {
       if ((rc = x->trace.ensure((size_t)bc * 8 * 8))) return rc;
@@ -2046,8 +2044,6 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
       fa.trace = (uint64_t*)x->trace.p;
     }
     if ((rc = timed(x, K_FIN, s, [&] { return launch_finalize(fa, s); }))) return rc;
-    static const bool fin_twice = ab_env("BB_FIN_TWICE") != nullptr;  // probe: warm second launch
-    if (fin_twice && (rc = timed(x, K_FIN, s, [&] { return launch_finalize(fa, s); }))) return rc;
     if (fin_trace) {  // finalize phases: keys loaded, table ready, content blended, CF-only, end
       std::vector<uint64_t> tr((size_t)bc * 8);
       BB_HIP(hipMemcpyAsync(tr.data(), x->trace.p, tr.size() * 8, hipMemcpyDeviceToHost, s));
@@ -2060,15 +2056,13 @@ int search_locked(bb_index* x, const bb_query* q, bb_result* res, bool allow_str
         if (!t[5] || !t[4]) continue;
         ++rows;
         for (int j = 1; j < 6; ++j) acc[j] += (double)(t[j] - t[0]);
-        acc[6] += (double)(t[7] - t[6]) * 100.0 / (double)std::max<uint64_t>(t[5] - t[0], 1);  // shader MHz
         t0 = std::min(t0, t[0]);
         t1 = std::max(t1, t[5]);
       }
       rows = std::max(rows, 1);
-      fprintf(stderr, "[bb finalize trace] rows=%d shader clock %.0f MHz us-from-start: keys %.2f table %.2f content %.2f "
-              "cf-only %.2f end %.2f | %.0f  span %.2f us\n", rows, acc[6] / rows, acc[1] / rows / 100,
-              acc[2] / rows / 100, acc[3] / rows / 100, acc[4] / rows / 100, acc[5] / rows / 100, acc[7] / rows / 100,
-              (double)(t1 - t0) / 100);
+      fprintf(stderr, "[bb finalize trace] rows=%d us-from-start: keys %.2f table %.2f content %.2f cf-only %.2f end %.2f  "
+              "span %.2f us\n", rows, acc[1] / rows / 100, acc[2] / rows / 100, acc[3] / rows / 100, acc[4] / rows / 100,
+              acc[5] / rows / 100, (double)(t1 - t0) / 100);
     }
   }
   if (stream) {

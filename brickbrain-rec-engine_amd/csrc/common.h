@@ -428,7 +428,6 @@ struct FinalizeArgs {
   int32_t* counts;          // [B] or null
   uint64_t* trace;          // probe runs (BB_SELECT_TRACE): per-row phase stamps, or null
   const uint32_t* idmap;    // packed-row positions -> global ids (SelectArgs.idmap), or null
-  int32_t abl;              // A/B probes only (BB_FIN_ABL): 1 = stop after the list loads, 2 = empty
 };
 __device__ __forceinline__ int64_t out_id(const uint32_t* idmap, uint32_t g) {
   return idmap ? (int64_t)idmap[g] : (int64_t)g;

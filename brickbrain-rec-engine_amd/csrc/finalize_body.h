@@ -49,7 +49,6 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
     if (a.trace && tid == 0) a.trace[q * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  if (a.trace && tid == 0) a.trace[q * 8 + 6] = __builtin_amdgcn_s_memtime();  // probe: shader clock
   // both side lists into registers first: a barrier waits for every outstanding load, so
   // loads issued after the setup barrier would add a second memory round trip (r04r trace:
   // 5.9 us until the lists were in LDS)
@@ -62,10 +61,6 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
       const int i = tid + j * NT;
       kv[side][j] = side < a.sides && i < a.K_int ? (side ? k1 : k0)[i] : 0ull;
     }
-  if (a.abl == 1) {
-    if (kv[0][0] == 1ull && kv[1][0] == 1ull) a.scores[0] = 0.f;  // (keeps the loads)
-    return;
-  }
   if (tid < 2) nnz[tid] = 0;
   if (tid == 0) {
     n_ent = 0;
@@ -90,7 +85,6 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
     if (side < a.sides && cnt_local[side]) atomicAdd(&nnz[side], cnt_local[side]);
   __syncthreads();
   stamp(1);
-  if (a.abl == 3) return;  // (A/B probe: stop here)
   int start[2] = {0, 0}, c[2] = {0, 0};
 #pragma unroll
   for (int side = 0; side < 2; ++side) {
@@ -134,7 +128,6 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   for (int j = tid; j < c[1]; j += NT) used[j] = 0;
   __syncthreads();
   stamp(2);
-  if (a.abl == 4) return;  // (A/B probe: stop here)
   auto slot0 = [](uint32_t g) { return (int)((g * 2654435761u) >> 22) & (kTab - 1); };
   for (int j = tid; j < c[1]; j += NT) {
     const uint32_t g = gid_of(L1[j]);
@@ -166,7 +159,6 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   }
   __syncthreads();
   stamp(3);
-  if (a.abl == 5) return;  // (A/B probe: stop here)
   // sample S for the pruning bound below: the first content entries (L0 order: the best
   // content scores, blended), topped up with the best CF-only entries (L1 order) when the
   // content list is short — at most kSamp together.  (The two side lists of a selective
@@ -186,7 +178,6 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   }
   __syncthreads();
   stamp(4);
-  if (a.abl == 6) return;  // (A/B probe: stop here)
   const int ne = c[0] + n_ent;
   const int n = ne < a.k ? ne : a.k;
   // Pruning bound (exact): T = the k-th largest f32 image in the sample S.  At least k
@@ -237,10 +228,9 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
     const uint32_t g = eg[e], hh = ehi[e];
     // the output id (a packed search maps slots through idmap: a global gather) is loaded
     // before the count, so its latency hides under it instead of following it
-    const int64_t oid = a.abl == 9 ? (int64_t)g : out_id(a.idmap, g);
-    int gt = 0, ge = 0, f = a.abl == 8 ? nsv : 0;
-    const int nsv_c = a.abl == 12 ? (nsv < 16 ? nsv : 16) : nsv;  // (A/B probe: one block)
-    for (; f + 16 <= nsv_c; f += 16) {
+    const int64_t oid = out_id(a.idmap, g);
+    int gt = 0, ge = 0, f = 0;
+    for (; f + 16 <= nsv; f += 16) {
       uint32_t kk[16];
 #pragma unroll
       for (int j = 0; j < 4; ++j) *(uint4*)(kk + 4 * j) = *(const uint4*)(sv_h + f + 4 * j);
@@ -250,18 +240,18 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
         ge += kk[j] >= hh;
       }
     }
-    for (; f < nsv_c; ++f) {
+    for (; f < nsv; ++f) {
       gt += sv_h[f] > hh;
       ge += sv_h[f] >= hh;
     }
-    int rank = a.abl == 8 ? si : gt;
+    int rank = gt;
     if (ge - gt > 1) {
       for (int f = 0; f < nsv; ++f) {
         const int x = sv_e[f];
         rank += sv_h[f] == hh && ((ek[x] > hk) || (ek[x] == hk && eg[x] < g));
       }
     }
-    if (rank < a.k && a.abl != 7) {
+    if (rank < a.k) {
       sc[rank] = (float)eh[e];
       id[rank] = oid;
     }
@@ -273,7 +263,6 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   if (a.counts && tid == 0) a.counts[q] = n;
   __syncthreads();
   stamp(5);
-  if (a.trace && tid == 0) a.trace[q * 8 + 7] = __builtin_amdgcn_s_memtime();
 }
 
 

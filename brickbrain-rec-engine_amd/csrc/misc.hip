@@ -200,7 +200,6 @@ __global__ __launch_bounds__(kFinThreads) void finalize1_kernel(FinalizeArgs a) 
 constexpr int kFinSmallK = 64;
 __global__ __launch_bounds__(64) void finalize1_small_kernel(FinalizeArgs a) {
   const int q = blockIdx.x;
-  if (a.abl == 2) return;
   finalize1_body<kFinSmallK, 64>(a, q, a.keys + (size_t)q * a.K_int, a.keys + ((size_t)a.B + q) * a.K_int,
                                  a.drop_rank0 && a.max_keys ? a.max_keys[q] : 0ull);
 }
