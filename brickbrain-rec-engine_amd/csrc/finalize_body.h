@@ -44,6 +44,8 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   __shared__ uint32_t samp[kSamp];
   __shared__ int n_samp_cf, n_surv;
   __shared__ uint32_t prune_t;
+  __shared__ int claim[2 * KC];         // survivors per strictly-greater count (ties, below)
+  __shared__ uint16_t rk[2 * KC];       // each survivor's strictly-greater count
   const int tid = threadIdx.x;
   auto stamp = [&](int slot) {  // probe-only phase timeline (s_memrealtime, 100 MHz)
     if (a.trace && tid == 0) a.trace[q * 8 + slot] = __builtin_amdgcn_s_memrealtime();
@@ -210,6 +212,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
   uint32_t* sv_h = tab_g;
   uint16_t* sv_e = tab_j;
   const uint32_t T = prune_t;
+  for (int i = tid; i < ne; i += NT) claim[i] = 0;
   for (int e = tid; e < ne; e += NT)
     if (ehi[e] >= T) {
       const int si = atomicAdd(&n_surv, 1);
@@ -217,35 +220,38 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
       sv_e[si] = (uint16_t)e;
     }
   __syncthreads();
-  const int nsv = n_surv;
-  // output position = rank under (h desc, id asc), counted on the order image of the f32
-  // rounding of h first (monotonic in h; 16 survivors per round from four ds_read_b128
-  // broadcasts): entries above are better, below worse.  Only survivors sharing that image
-  // with others (ties and near-ties, rare) take the full (h, id) comparison among them.
+  const int nsv = n_surv, nsp = (nsv + 15) & ~15;
+  for (int i = nsv + tid; i < nsp; i += NT) sv_h[i] = 0u;  // pad to whole blocks: image 0 ranks below every entry
+  __syncthreads();
+  // output position = rank under (h desc, id asc).  First the count of survivors with a
+  // strictly larger f32 image of h (monotonic in h; 16 per round from four ds_read_b128
+  // broadcasts).  Survivors sharing an image get the same count — and only they do (a larger
+  // image is counted by the smaller one's count) — so a claim table on the counts finds the
+  // ties and near-ties (rare), which then take the full (h, id) comparison among themselves.
+  // (One survivor per thread: a second round of the count doubled the phase, rank_probe.)
+  int64_t oid_pf = 0;  // the output id of survivor tid (an idmap gather), loaded ahead of the count
   for (int si = tid; si < nsv; si += NT) {
-    const int e = sv_e[si];
-    const uint64_t hk = ek[e];
-    const uint32_t g = eg[e], hh = ehi[e];
-    // the output id (a packed search maps slots through idmap: a global gather) is loaded
-    // before the count, so its latency hides under it instead of following it
-    const int64_t oid = out_id(a.idmap, g);
-    int gt = 0, ge = 0, f = 0;
-    for (; f + 16 <= nsv; f += 16) {
+    const uint32_t hh = sv_h[si];
+    if (si == tid) oid_pf = out_id(a.idmap, eg[sv_e[si]]);
+    int gt = 0;
+    for (int f = 0; f < nsp; f += 16) {
       uint32_t kk[16];
 #pragma unroll
       for (int j = 0; j < 4; ++j) *(uint4*)(kk + 4 * j) = *(const uint4*)(sv_h + f + 4 * j);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        gt += kk[j] > hh;
-        ge += kk[j] >= hh;
-      }
+      for (int j = 0; j < 16; ++j) gt += kk[j] > hh;
     }
-    for (; f < nsv; ++f) {
-      gt += sv_h[f] > hh;
-      ge += sv_h[f] >= hh;
-    }
+    rk[si] = (uint16_t)gt;
+    atomicAdd(&claim[gt], 1);
+  }
+  __syncthreads();
+  for (int si = tid; si < nsv; si += NT) {
+    const int e = sv_e[si];
+    const int gt = rk[si];
     int rank = gt;
-    if (ge - gt > 1) {
+    if (claim[gt] > 1) {
+      const uint64_t hk = ek[e];
+      const uint32_t g = eg[e], hh = ehi[e];
       for (int f = 0; f < nsv; ++f) {
         const int x = sv_e[f];
         rank += sv_h[f] == hh && ((ek[x] > hk) || (ek[x] == hk && eg[x] < g));
@@ -253,7 +259,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
     }
     if (rank < a.k) {
       sc[rank] = (float)eh[e];
-      id[rank] = oid;
+      id[rank] = si == tid ? oid_pf : out_id(a.idmap, eg[e]);
     }
   }
   for (int i = n + tid; i < a.k; i += NT) {

@@ -204,13 +204,14 @@ __global__ __launch_bounds__(64) void finalize1_small_kernel(FinalizeArgs a) {
                                  a.drop_rank0 && a.max_keys ? a.max_keys[q] : 0ull);
 }
 
-// Side lists of <= 128 keys (k_side = 2k up to k = 63: the configs[2] hybrid's 101): two
-// waves per row and ≈10 KiB of LDS — the 512-key instance's ≈39 KiB held four rows per CU,
-// so 1,024 rows did not start in one round.
+// Side lists of <= 128 keys (k_side = 2k up to k = 63: the configs[2] hybrid's 101): ≈13 KiB
+// of LDS per row instead of the 512-key instance's ≈41 KiB, so the other in-flight batches'
+// kernels keep room on every CU (configs[2] 22.7 -> 24.5-25.3 M q/s), and four waves, so
+// the rank count takes each of its <= 256 survivors in one round.
 constexpr int kFinMidK = 128;
-__global__ __launch_bounds__(128) void finalize1_mid_kernel(FinalizeArgs a) {
+__global__ __launch_bounds__(256) void finalize1_mid_kernel(FinalizeArgs a) {
   const int q = blockIdx.x;
-  finalize1_body<kFinMidK, 128>(a, q, a.keys + (size_t)q * a.K_int, a.keys + ((size_t)a.B + q) * a.K_int,
+  finalize1_body<kFinMidK, 256>(a, q, a.keys + (size_t)q * a.K_int, a.keys + ((size_t)a.B + q) * a.K_int,
                                 a.drop_rank0 && a.max_keys ? a.max_keys[q] : 0ull);
 }
 
@@ -466,7 +467,7 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   if (a.P == 1 && !legacy && a.K_int <= kFinSmallK && !wide)
     bb_launch(finalize1_small_kernel, dim3(a.n_rows), dim3(64), 0, s, a);
   else if (a.P == 1 && !legacy && a.K_int <= kFinMidK && !wide)
-    bb_launch(finalize1_mid_kernel, dim3(a.n_rows), dim3(128), 0, s, a);
+    bb_launch(finalize1_mid_kernel, dim3(a.n_rows), dim3(256), 0, s, a);
   else if (a.P == 1 && !legacy)
     bb_launch(finalize1_kernel, dim3(a.n_rows), dim3(kFinThreads), 0, s, a);
   else
