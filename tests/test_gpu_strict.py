@@ -182,3 +182,38 @@ def test_strict_c2_hybrid_b1024_every_query(brickrec):
         _assert_row(gate, sc[b], ids[b], cnt[b], hi, hs, k)
     gate.report(0.0)
     idx.close()
+
+
+@pytest.mark.parametrize("k", [20, 80])
+def test_strict_hybrid_finalize_instances(brickrec, k):
+    """finalize1's three list capacities (misc.hip): k = 20 -> side lists of 41 keys (the
+    one-wave 64-key instance), k = 50 above (the 128-key instance), k = 80 -> 161 keys (the
+    512-key instance) — each id-exact with the bits of f32(h) on configs[2]'s data, with the
+    constraint-first search (the selective mask) and without it (every row allowed)."""
+    import torch
+    from test_gpu_configs import _c2_data
+    x = R.unit_rows(N25, D25, 1234)
+    f, u, parts, year, theme, liked, rated = _c2_data()
+    B = 64
+    liked, u, rated = liked[:B], u[:B], rated[:B]
+    ks = 2 * k
+    idx = brickrec.ItemIndex(dtype="f32")
+    idx.upload_items(x)
+    idx.upload_cf(f)
+    idx.upload_attrs(parts, year, theme)
+    dev = torch.device("cuda", 0)
+    rows = idx.get_rows(np.arange(N25))
+    present = torch.ones(N25, dtype=torch.bool, device=dev)
+    for mask in (np.asarray(idx.eval_mask(brickrec.Predicate(parts_max=800, year_min=2015)), bool),
+                 np.ones(N25, bool)):
+        sc, ids, cnt = idx.search("hybrid", k, q_items=liked, q_cf=u, mask=mask, excl=rated)
+        m = torch.from_numpy(mask).to(dev)
+        ci, cs = _topk(_scores(rows, rows[liked]), m, ks, drop_rank0=present)
+        okf = m.unsqueeze(0) & ~torch.from_numpy(rated).to(dev)
+        fi, fs = _topk(_scores(f.astype(np.float32), u.astype(np.float32)), okf, ks)
+        gate = Gate(f"strict hybrid k={k} B={B} mask density {mask.mean():.3f}")
+        for b in range(B):
+            hi, hs = _blend(ci[b], cs[b], fi[b], fs[b], 0.4, 0.6, k)
+            _assert_row(gate, sc[b], ids[b], cnt[b], hi, hs, k)
+        gate.report(0.0)
+    idx.close()
