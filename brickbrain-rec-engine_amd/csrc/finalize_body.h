@@ -20,8 +20,10 @@ __device__ __forceinline__ double blend_h(double wc, double c, double wf, double
   return wc * c + wf * f;
 }
 
+// Order image of a blended h.  -0.0 is folded into +0.0 first (the Python sort compares them
+// equal; a -0.0 blend needs negative weights and two zero scores)
 __device__ __forceinline__ uint64_t ord64_of(double d) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, d);
+  const uint64_t u = __builtin_bit_cast(uint64_t, d + 0.0);
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
 
@@ -156,7 +158,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
     const double fs = hit >= 0 ? (double)float_of_ord(ordk_of(L1[hit])) : 0.0;
     eh[i] = blend_h(a.w_content, cs, a.w_cf, fs);
     ek[i] = ord64_of(eh[i]);
-    ehi[i] = ord_of((float)eh[i]);
+    ehi[i] = ord_of((float)eh[i] + 0.0f);
     eg[i] = g;
   }
   __syncthreads();
@@ -173,7 +175,7 @@ __device__ __forceinline__ void finalize1_body(const FinalizeArgs& a, int q, con
       const int pos = c[0] + atomicAdd(&n_ent, 1);
       eh[pos] = blend_h(a.w_content, 0.0, a.w_cf, (double)float_of_ord(ordk_of(L1[j])));
       ek[pos] = ord64_of(eh[pos]);
-      ehi[pos] = ord_of((float)eh[pos]);
+      ehi[pos] = ord_of((float)eh[pos] + 0.0f);
       eg[pos] = g;
       if (j < kSamp - c0s) samp[c0s + atomicAdd(&n_samp_cf, 1)] = ehi[pos];
     }

@@ -182,3 +182,43 @@ def test_constraint_first_equivalence():
             fs = np.where(real, (f @ u)[np.maximum(slots, 0)], -np.inf)
             got_slot, _ = R.topk_indices(fs, k, real & ~rated[np.maximum(slots, 0)])
             assert list(slots[got_slot]) == list(want_i)
+
+
+def test_finalize_pruned_rank_equals_full_rank():
+    """finalize_body.h's ranking, restated on the host: the pruning bound T (the k-th largest
+    f32 image among a sample of the entries) drops only entries that rank >= k, and the
+    survivors' ranks — the count of strictly larger images, plus, where the claim table finds
+    a shared count, the (h desc, id asc) comparison among equal images — equal their ranks
+    among all entries.  Heavy ties (h rounded to a coarse grid, duplicate f32 images of
+    distinct f64 h) and every sample size around k."""
+    rng = np.random.default_rng(5)
+    for trial in range(300):
+        n = int(rng.integers(1, 220))
+        k = int(rng.integers(1, 80))
+        h = rng.normal(0.0, 0.2, n)
+        if trial % 3 == 0:
+            h = np.round(h * 16) / 16                      # exact ties
+        if trial % 3 == 1:
+            h = h.astype(np.float32).astype(np.float64) + rng.integers(0, 2, n) * 1e-12  # equal f32, distinct f64
+        h = h + 0.0   # (no -0.0: the device's scores are +0-folded, rr_key, so no blend is -0.0)
+        g = rng.permutation(100000)[:n].astype(np.int64)   # ids
+        img = np.float32(h).view(np.uint32)
+        img = np.where(img & 0x80000000, ~img, img | 0x80000000).astype(np.uint64)   # ord_of
+        true_order = sorted(range(n), key=lambda e: (-h[e], g[e]))
+        true_rank = np.empty(n, int)
+        true_rank[true_order] = np.arange(n)
+        ns = int(min(n, rng.integers(0, 70)))
+        samp = rng.choice(n, ns, replace=False)
+        T = 0
+        if ns >= k:
+            T = int(np.sort(img[samp])[::-1][k - 1])
+        surv = np.flatnonzero(img >= T)
+        assert np.all(true_rank[img < T] >= k)
+        gt = np.array([(img[surv] > img[e]).sum() for e in surv])
+        claim = np.bincount(gt, minlength=len(surv) + 1)
+        for j, e in enumerate(surv):
+            r = gt[j]
+            if claim[gt[j]] > 1:
+                same = surv[img[surv] == img[e]]
+                r += sum(1 for x in same if h[x] > h[e] or (h[x] == h[e] and g[x] < g[e]))
+            assert r == true_rank[e], (trial, e)
