@@ -64,7 +64,7 @@ def unit_rows(n, d, seed, dev, chunk=1 << 20):
     return out
 
 
-def run_case(name, c, seconds, dev, stream=-1, inflight=1):
+def run_case(name, c, seconds, dev, stream=-1, inflight=1, refine=-1):
     import torch
     import brickrec
     n, d, B, k, dt = c["n"], c["d"], c["B"], c["k"], c["dtype"]
@@ -72,12 +72,14 @@ def run_case(name, c, seconds, dev, stream=-1, inflight=1):
     idx = brickrec.ItemIndex(device=dev.index, dtype=dt)
     idx.upload_items(x, prenormalized=True)
     idx.set_option("stream", stream)
+    idx.set_option("stream_refine", refine)
     # extra lanes for the in-flight throughput (bench.py's scheme): own handle, stream, copy
     lanes = []
     for j in range(1, inflight):
         lj = brickrec.ItemIndex(device=dev.index, dtype=dt)
         lj.upload_items(x, prenormalized=True)
         lj.set_option("stream", stream)
+        lj.set_option("stream_refine", refine)
         lanes.append(lj)
     del x
     torch.cuda.empty_cache()
@@ -134,7 +136,7 @@ def run_case(name, c, seconds, dev, stream=-1, inflight=1):
     launches = {kk: v["launches"] // ps for kk, v in prof.items() if v["launches"]}
     gemm_us = kern.get("gemm", 0.0)
     peak = F32_TF if dt == "f32" else BF16_TF
-    out = {"case": name, **{kk: v for kk, v in c.items()}, "stream_opt": stream, "steps": steps,
+    out = {"case": name, **{kk: v for kk, v in c.items()}, "stream_opt": stream, "refine_opt": refine, "steps": steps,
            "qps": round(B * steps / el, 1), "ms_per_batch": round(1e3 * el / steps, 4),
            "p50_ms": round(float(np.median(lat)), 4),
            "kernels_us_per_batch": kern, "launches_per_batch": launches,
@@ -175,13 +177,14 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--stream", type=int, default=-1, help="-1 auto, 0 slab path, 1 streaming top-K")
     ap.add_argument("--inflight", type=int, default=1, help="also measure with this many batches in flight")
+    ap.add_argument("--refine", type=int, default=-1, help="stream_refine: -1 auto, 0 off, 1 the two-level bound")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     f = open(args.out, "a") if args.out else None
     for name in args.cases.split(","):
-        res = run_case(name, CASES[name], args.seconds, dev, args.stream, args.inflight)
+        res = run_case(name, CASES[name], args.seconds, dev, args.stream, args.inflight, args.refine)
         line = json.dumps(res)
         print(line, flush=True)
         if f:
