@@ -438,29 +438,6 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   // f16 operands: the re-rank copy of an f32 index (kScanF16); bf16 otherwise
   constexpr bool F16 = (ABL & kScanF16) != 0;
   static_assert(!F16 || sizeof(T) == 2, "f16 operands are 16-bit");
-  uint4 qf[U];
-  const float hq_raw = scan2_load_queries<T, KU, F16>(a, q, h, qf, chunk == 0 && a.q_istats != nullptr);
-  float qa[sizeof(T) == 4 ? 4 * U : 1];  // f32: the operand as 4U scalars, pinned to AGPRs
-  if constexpr (sizeof(T) == 4) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      qa[4 * u + 0] = __uint_as_float(qf[u].x);
-      qa[4 * u + 1] = __uint_as_float(qf[u].y);
-      qa[4 * u + 2] = __uint_as_float(qf[u].z);
-      qa[4 * u + 3] = __uint_as_float(qf[u].w);
-    }
-#pragma unroll
-    for (int i = 0; i < 4 * U; ++i) asm volatile("" : "+a"(qa[i]));
-  }
-  u32x4v qv[sizeof(T) == 2 ? U : 1];  // bf16: the operand as 4-dword vectors, pinned to AGPRs
-  if constexpr (sizeof(T) == 2) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      qv[u] = __builtin_bit_cast(u32x4v, qf[u]);
-      asm volatile("" : "+a"(qv[u]));
-    }
-  }
-
   // LDS fragment bases: chunk (2u + h) ^ swz(r) of row r = rd[u % G] + (u / G)·G·32 bytes
   const int swz = scan_swz<KU>(r);
   int rd[G];
@@ -488,6 +465,40 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + buf * TILE_B + (wave * PIECES + p) * 1024);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src) : "memory");
   };
+
+  // The first two tiles' LDS-DMA goes out before the query operand's loads, so the item
+  // rows' latency overlaps the queries' instead of following it (the queries are pinned to
+  // AGPRs below, a wait that now also retires these pieces; nothing reads LDS before the
+  // explicit wait + barrier ahead of the first tile).
+#pragma unroll
+  for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
+  {
+    const int t1 = tile_lo + 1 < tile_hi ? tile_lo + 1 : tile_lo;
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) stage_piece(t1, 1, p);
+  }
+  uint4 qf[U];
+  const float hq_raw = scan2_load_queries<T, KU, F16>(a, q, h, qf, chunk == 0 && a.q_istats != nullptr);
+  float qa[sizeof(T) == 4 ? 4 * U : 1];  // f32: the operand as 4U scalars, pinned to AGPRs
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      qa[4 * u + 0] = __uint_as_float(qf[u].x);
+      qa[4 * u + 1] = __uint_as_float(qf[u].y);
+      qa[4 * u + 2] = __uint_as_float(qf[u].z);
+      qa[4 * u + 3] = __uint_as_float(qf[u].w);
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * U; ++i) asm volatile("" : "+a"(qa[i]));
+  }
+  u32x4v qv[sizeof(T) == 2 ? U : 1];  // bf16: the operand as 4-dword vectors, pinned to AGPRs
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      qv[u] = __builtin_bit_cast(u32x4v, qf[u]);
+      asm volatile("" : "+a"(qv[u]));
+    }
+  }
 
   const size_t w0 = (size_t)(a.slab_start >> 5);
   const uint32_t* erow = a.excl + (size_t)(q < a.M_valid ? q : a.M_valid - 1) * a.excl_ld;
@@ -531,14 +542,8 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   const size_t region = ((size_t)q * n_chunks + chunk) * 2 + h;
   if constexpr (STREAM) stream_begin(a, q, region, sl);
 
-  // first tile
-#pragma unroll
-  for (int p = 0; p < PIECES; ++p) stage_piece(tile_lo, 0, p);
-  {
-    const int t1 = tile_lo + 1 < tile_hi ? tile_lo + 1 : tile_lo;
-#pragma unroll
-    for (int p = 0; p < PIECES; ++p) stage_piece(t1, 1, p);
-  }
+  // (the first two tiles' LDS-DMA was issued before the query loads, above: both latencies
+  // overlap; this wait retires them all)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   asm volatile("s_nop 4");
