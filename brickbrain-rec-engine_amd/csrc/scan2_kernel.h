@@ -477,6 +477,14 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
 #pragma unroll
     for (int p = 0; p < PIECES; ++p) stage_piece(t1, 1, p);
   }
+  // the query's code quantum (prep wrote it with the operand) is loaded ahead of the operand
+  // too: one memory round trip for the whole prologue instead of two
+  constexpr bool kHs = ((ABL & kScanS16) != 0 || (ABL & kScanList) != 0) && (ABL & kScanStream) == 0;
+  float hs_pre = 0.f;
+  if constexpr (kHs) {
+    constexpr bool kS16b = (ABL & kScanS16) != 0;  // (the image path reads it whatever the prologue)
+    if ((kS16b || !a.q_raw) && q < a.M_valid) hs_pre = a.s_h[q];
+  }
   uint4 qf[U];
   const float hq_raw = scan2_load_queries<T, KU, F16>(a, q, h, qf, chunk == 0 && a.q_istats != nullptr);
   float qa[sizeof(T) == 4 ? 4 * U : 1];  // f32: the operand as 4U scalars, pinned to AGPRs
@@ -511,7 +519,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   constexpr bool S16 = (ABL & kScanS16) != 0 && !STREAM;
   float sk = 0.f;
   if constexpr (S16) {
-    const float hq = q < a.M_valid ? a.s_h[q] : 0.f;
+    const float hq = hs_pre;  // (a.s_h[q] for q < M_valid, loaded above)
     sk = hq > 0.f ? 1.0f / (hq * 32767.f) : 0.f;
     asm volatile("" : "+v"(sk));  // consumed before any LDS-DMA is in flight
   }
@@ -520,7 +528,7 @@ __global__ __launch_bounds__(kScanWaves * 64, 1) void scan2_kernel(GemmArgs a, i
   constexpr bool LIST = (ABL & kScanList) != 0 && !STREAM && !S16;
   float k2 = 0.f;
   if constexpr (LIST) {
-    const float hq = a.q_raw ? hq_raw : q < a.M_valid ? a.s_h[q] : 0.f;
+    const float hq = a.q_raw ? hq_raw : hs_pre;
     k2 = hq > 0.f ? 1.0f / (hq * 65535.f) : 0.f;
     asm volatile("" : "+v"(k2));  // consumed before any LDS-DMA is in flight
   }
