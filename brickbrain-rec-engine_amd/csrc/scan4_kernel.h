@@ -263,6 +263,30 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     for (int p = 0; p < PIECES; ++p) stage_piece(t1, 1, p);
   }
 
+  // The prologue's other loads go out with the first tiles, ahead of the query operand — the
+  // code quanta, the streaming bounds and the first tile's eligibility words — so the whole
+  // prologue is the operand's round trips, not one more after them (the operand's pinning
+  // waits retire these too: loads complete in order).
+  constexpr bool S16 = (ABL & kScanS16) != 0 && !STREAM;
+  constexpr bool LIST = (ABL & kScanList) != 0 && !STREAM && !S16;
+  float hsA = 0.f, hsB = 0.f;
+  if constexpr (S16 || LIST) {
+    hsA = qA < a.M_valid ? a.s_h[qA] : 0.f;
+    hsB = qB < a.M_valid ? a.s_h[qB] : 0.f;
+  }
+  uint64_t tkA = 0ull, tkB = 0ull;
+  if constexpr (STREAM) {
+    if (qA < a.M_valid) tkA = a.thr_keys[(size_t)qA * a.thr_ld + a.thr_ld - 1];
+    if (qB < a.M_valid) tkB = a.thr_keys[(size_t)qB * a.thr_ld + a.thr_ld - 1];
+  }
+  const size_t w0 = (size_t)(a.slab_start >> 5);
+  const uint32_t* erowA = a.excl + (size_t)(qA < a.M_valid ? qA : a.M_valid - 1) * a.excl_ld;
+  const uint32_t* erowB = a.excl + (size_t)(qB < a.M_valid ? qB : a.M_valid - 1) * a.excl_ld;
+  // eligibility words of the current tile (pw, mw, ewA, ewB) and of the previous tile for
+  // block B's deferred epilogue (ppw, pmw, pewB)
+  uint32_t pw = a.present[w0 + tile_lo], mw = a.mask[w0 + tile_lo], ewA = erowA[w0 + tile_lo],
+           ewB = erowB[w0 + tile_lo];
+
   // queries: block A (qA), block B (qB); register j = b·U + u lives in an AGPR iff j < NA
   u32x4v qv[2 * U];
   {
@@ -311,15 +335,11 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
     }
   }
 
-  const size_t w0 = (size_t)(a.slab_start >> 5);
-  const uint32_t* erowA = a.excl + (size_t)(qA < a.M_valid ? qA : a.M_valid - 1) * a.excl_ld;
-  const uint32_t* erowB = a.excl + (size_t)(qB < a.M_valid ? qB : a.M_valid - 1) * a.excl_ld;
   float* park = (float*)(smem + RING * TILE_B) + wave * 1024;
   // int16 score image (kScanS16): code scales 1/(h·32767) of the two query blocks
-  constexpr bool S16 = (ABL & kScanS16) != 0 && !STREAM;
   float skA = 0.f, skB = 0.f;
   if constexpr (S16) {
-    const float hA = qA < a.M_valid ? a.s_h[qA] : 0.f, hB = qB < a.M_valid ? a.s_h[qB] : 0.f;
+    const float hA = hsA, hB = hsB;
     skA = hA > 0.f ? 1.0f / (hA * 32767.f) : 0.f;
     skB = hB > 0.f ? 1.0f / (hB * 32767.f) : 0.f;
   }
@@ -327,11 +347,10 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   // code scale 1/(65535·h), the lane's top-5 of the current period and the rank-0 top-2.  A
   // finished period's lists are packed and stored at the start of the NEXT tile body, ahead
   // of its DMA pieces, so the end-of-tile vmcnt wait never waits for a store's round trip.
-  constexpr bool LIST = (ABL & kScanList) != 0 && !STREAM && !S16;
   static_assert(!LIST || IL, "list epilogue: interleaved schedule (rows up to 512 wide) only");
   float k2A = 0.f, k2B = 0.f;
   if constexpr (LIST) {
-    const float hA = qA < a.M_valid ? a.s_h[qA] : 0.f, hB = qB < a.M_valid ? a.s_h[qB] : 0.f;
+    const float hA = hsA, hB = hsB;
     k2A = hA > 0.f ? 1.0f / (hA * 65535.f) : 0.f;
     k2B = hB > 0.f ? 1.0f / (hB * 65535.f) : 0.f;
   }
@@ -375,20 +394,16 @@ __device__ __forceinline__ void scan4_body(const GemmArgs& a, int n_chunks, int 
   if constexpr (STREAM) {  // bound = the last key of the query's pilot list (stream_begin)
     // (an image at or below ord(-inf) takes every finite score: thrf = -inf)
     if (qA < a.M_valid) {
-      const uint32_t o = ordk_of(a.thr_keys[(size_t)qA * a.thr_ld + a.thr_ld - 1]);
+      const uint32_t o = ordk_of(tkA);
       slA.thr = o ? o : 1u;
       slA.thrf = slA.thr <= 0x007FFFFFu ? -__builtin_inff() : float_of_ord(slA.thr);
     }
     if (qB < a.M_valid) {
-      const uint32_t o = ordk_of(a.thr_keys[(size_t)qB * a.thr_ld + a.thr_ld - 1]);
+      const uint32_t o = ordk_of(tkB);
       slB.thr = o ? o : 1u;
       slB.thrf = slB.thr <= 0x007FFFFFu ? -__builtin_inff() : float_of_ord(slB.thr);
     }
   }
-  // eligibility words of the current tile (pw, mw, ewA, ewB) and of the previous tile for
-  // block B's deferred epilogue (ppw, pmw, pewB)
-  uint32_t pw = a.present[w0 + tile_lo], mw = a.mask[w0 + tile_lo], ewA = erowA[w0 + tile_lo],
-           ewB = erowB[w0 + tile_lo];
   uint32_t ppw = 0, pmw = 0, pewB = 0, nw_p = 0, nw_m = 0, nw_eA = 0, nw_eB = 0;
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
